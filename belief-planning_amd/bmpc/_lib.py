@@ -1,0 +1,96 @@
+"""Loader of the HIP library ``libbmpc.so`` (the product path; there is no CPU fallback).
+
+``build()`` compiles it in-tree for gfx950 with hipcc; ``lib()`` loads it and raises
+``BmpcUnavailable`` when it is missing or no HIP device is usable.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+SO_PATH = os.path.join(PKG_DIR, "libbmpc.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("BMPC_OFFLOAD_ARCH", "gfx950")
+
+
+class BmpcUnavailable(RuntimeError):
+    """libbmpc.so (the MI355X kernels) cannot be loaded or has no usable HIP device."""
+
+
+def sources():
+    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_plan.cpp")]
+
+
+def headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    return hs + [os.path.join(INCLUDE, "bmpc.h")]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libbmpc.so for gfx950 (in-tree) if missing or stale."""
+    if not force and os.path.exists(SO_PATH):
+        newest = max(os.path.getmtime(p) for p in sources() + headers())
+        if os.path.getmtime(SO_PATH) >= newest:
+            return SO_PATH
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
+           "-I" + INCLUDE, "-I" + CSRC, *sources(), "-o", SO_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(SO_PATH + ".tmp", SO_PATH)
+    return SO_PATH
+
+
+_LIB = None
+
+_SIGS = {
+    "bmpc_last_error": (C.c_char_p, []),
+    "bmpc_abi_version": (C.c_int, []),
+    "bmpc_open": (C.c_int, [C.c_int, C.c_void_p]),
+    "bmpc_close": (C.c_int, [C.c_void_p]),
+    "bmpc_plan_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "bmpc_plan_destroy": (C.c_int, [C.c_void_p]),
+    "bmpc_plan_info": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "bmpc_set_policies": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "bmpc_reset": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "bmpc_solve": (C.c_int, [C.c_void_p] + [C.c_void_p] * 9),
+    "bmpc_solve_device": (C.c_int, [C.c_void_p] + [C.c_void_p] * 10),
+    "bmpc_get_tree": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
+    "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def load(path: str = SO_PATH):
+    """Load a libbmpc.so and declare the C ABI (no device access)."""
+    if not os.path.exists(path):
+        raise BmpcUnavailable(f"{path} not built; run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = load()
+    return _LIB
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().bmpc_last_error().decode(errors="replace")
+        raise BmpcUnavailable(f"{what} failed ({rc}): {msg}") if rc in (-19, -5, -12) else RuntimeError(
+            f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,118 @@
+"""Python handle over a libbmpc plan: one batch of egos sharing one controller/model."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from ._lib import check, lib
+
+_CTX = {}
+
+
+def context(device: int = 0):
+    """One bmpc_ctx per HIP device per process."""
+    if device not in _CTX:
+        h = C.c_void_p()
+        check(lib().bmpc_open(device, C.byref(h)), "bmpc_open")
+        _CTX[device] = h
+    return _CTX[device]
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class BatchPlan:
+    """A batch of ``batch`` independent egos, each with its own scenario tree, warm start
+    and policy set, solved together by one kernel launch per phase."""
+
+    def __init__(self, desc: abi.PlanDesc, batch: int, device: int = 0):
+        self.desc = desc
+        self.batch = int(batch)
+        self.device = device
+        self._ctx = context(device)
+        h = C.c_void_p()
+        check(lib().bmpc_plan_create(self._ctx, C.byref(desc), self.batch, C.byref(h)), "bmpc_plan_create")
+        self._h = h
+        info = np.zeros(abi.INFO_COUNT, np.int32)
+        check(lib().bmpc_plan_info(h, _p(info)), "bmpc_plan_info")
+        self.info = info
+        self.T, self.U = int(info[abi.INFO_T]), int(info[abi.INFO_U])
+        self.bdim, self.nbranch = int(info[abi.INFO_BDIM]), int(info[abi.INFO_NBRANCH])
+        self.nv, self.neq = int(info[abi.INFO_NV]), int(info[abi.INFO_NEQ])
+        self.nrows, self.ncones = int(info[abi.INFO_NROWS]), int(info[abi.INFO_NCONES])
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bmpc_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- state ----------------------------------------------------------------------------
+    def set_policies(self, rows, mask=None):
+        """rows: per ego, m (kind, params) tuples (``update_backup``)."""
+        arr = abi.policy_array(rows)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_set_policies(self._h, arr, _p(m)), "bmpc_set_policies")
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_reset(self._h, _p(m)), "bmpc_reset")
+
+    # ---- solves ---------------------------------------------------------------------------
+    def solve(self, x, z, xref):
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        x, z, xref = (np.ascontiguousarray(np.asarray(v, np.float64).reshape(B, n)) for v in (x, z, xref))
+        out = dict(upred=np.zeros((B, self.U, d)), xpred=np.zeros((B, self.T, n)),
+                   branch_w=np.zeros((B, self.nbranch - 1)), J=np.zeros(B),
+                   status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32))
+        check(lib().bmpc_solve(self._h, _p(x), _p(z), _p(xref), *(_p(out[k]) for k in
+                               ("upred", "xpred", "branch_w", "J", "status", "iters"))), "bmpc_solve")
+        return out
+
+    def solve_device(self, x_ptr, z_ptr, xref_ptr, upred_ptr=None, xpred_ptr=None, bw_ptr=None,
+                     J_ptr=None, status_ptr=None, iters_ptr=None, stream=None):
+        """Device-pointer variant (e.g. torch tensors' data_ptr()), asynchronous."""
+        vp = [C.c_void_p(p) if p else None for p in (x_ptr, z_ptr, xref_ptr, upred_ptr, xpred_ptr,
+                                                     bw_ptr, J_ptr, status_ptr, iters_ptr, stream)]
+        check(lib().bmpc_solve_device(self._h, *vp), "bmpc_solve_device")
+
+    def tree(self):
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),
+                   zbar=np.zeros((B, self.T, n)), w=np.zeros((B, self.nbranch)),
+                   p=np.zeros((B, self.bdim, self.desc.m)), sol=np.zeros((B, self.nv)))
+        check(lib().bmpc_get_tree(self._h, *(_p(out[k]) for k in ("xbar", "ubar", "zbar", "w", "p", "sol"))),
+              "bmpc_get_tree")
+        return out
+
+    # ---- timing ---------------------------------------------------------------------------
+    def enable_timing(self, on=True):
+        check(lib().bmpc_enable_timing(self._h, 1 if on else 0), "bmpc_enable_timing")
+
+    def timing(self):
+        ms = np.zeros(2)
+        cnt = C.c_int32()
+        check(lib().bmpc_timing(self._h, _p(ms), C.byref(cnt)), "bmpc_timing")
+        return dict(tree_ms=float(ms[0]), ipm_ms=float(ms[1]), count=int(cnt.value))
+
+
+def model_eval(desc: abi.PlanDesc, pol_rows, x, u, z, device: int = 0):
+    """Batched PredictiveModel evaluation on the GPU (parity entry)."""
+    x, u, z = (np.ascontiguousarray(np.atleast_2d(np.asarray(v, np.float64))) for v in (x, u, z))
+    B, n, d, m, N = x.shape[0], desc.n, desc.d, desc.m, desc.N
+    out = dict(A=np.zeros((B, n, n)), B=np.zeros((B, n, d)), C=np.zeros((B, n)), xp=np.zeros((B, n)),
+               p=np.zeros((B, m)), dp=np.zeros((B, m, n)), zpred=np.zeros((B, N, m * n)),
+               h0=np.zeros(B), dh=np.zeros((B, n)))
+    arr = abi.policy_array(pol_rows)
+    check(lib().bmpc_model_eval(context(device), C.byref(desc), arr, B, _p(x), _p(u), _p(z),
+                                *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh"))),
+          "bmpc_model_eval")
+    return out

@@ -1,0 +1,469 @@
+// bmpc_hip.hip -- gfx950 kernels and the C ABI of libbmpc.so (include/bmpc.h).
+//
+// Mapping: one 64-lane wavefront (one 64-thread workgroup) per ego.  Kernel 1 rebuilds the
+// ego's scenario tree (warm start, rollouts, linearisation, collision rows); kernel 2 runs
+// the structured HSDE interior-point solve and unpacks the solution.  All per-ego state
+// lives in one contiguous slab of HBM (Layout), so every strided lane loop reads and writes
+// contiguous 512-byte segments.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "bmpc_plan.h"
+#include "bmpc_solve.h"
+
+using namespace bmpc;
+
+namespace {
+
+struct DevExec {
+  int lane;
+  static constexpr int nlanes = 64;
+  __device__ void sync() const { __syncthreads(); }
+  __device__ double sum(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ double max(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ double min(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+};
+
+struct Bundle {
+  Plan P;
+  Layout L;
+};
+
+template <class M>
+__global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
+                                             const bmpc_policy* __restrict__ pol,
+                                             const double* __restrict__ x, const double* __restrict__ z,
+                                             const double* __restrict__ xref, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  DevExec ex{(int)threadIdx.x};
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  tree_update<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+}
+
+template <class M>
+__global__ __launch_bounds__(64) void k_ipm(const Bundle* __restrict__ B, double* __restrict__ ws,
+                                            const bmpc_policy* __restrict__ pol, double* upred,
+                                            double* xpred, double* bw, double* J, int32_t* status,
+                                            int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  DevExec ex{(int)threadIdx.x};
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r = solve_ego_ipm<DevExec, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += 64) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += 64) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += 64) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = w[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+}
+
+__global__ void k_gather(const double* __restrict__ ws, size_t stride, size_t off, int count,
+                         double* __restrict__ out, int batch) {
+  const size_t tot = (size_t)batch * count;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i / count, j = i % count;
+    out[i] = ws[e * stride + off + j];
+  }
+}
+
+__global__ void k_reset(double* ws, size_t stride, size_t off, const uint8_t* mask, int batch) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < batch && (!mask || mask[e])) ws[e * stride + off + MISC_INIT] = 0.0;
+}
+
+template <class M>
+__global__ void k_model(bmpc_plan_desc D, const bmpc_policy* pol, int B, const double* x,
+                        const double* u, const double* z, double* A, double* Bm, double* C,
+                        double* xp, double* p, double* dp, double* zpred, double* h0, double* dh) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int n = D.n, d = D.d, m = D.m, N = D.N;
+#define OFF(ptr, k) (ptr ? ptr + (size_t)b * (k) : nullptr)
+  model_eval_point<M>(D, pol + (size_t)b * m, x + b * n, u + b * d, z + b * n, OFF(A, n * n),
+                      OFF(Bm, n * d), OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),
+                      OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n));
+#undef OFF
+}
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHECK(expr)                                                                      \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) return fail(-5, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+}  // namespace
+
+struct bmpc_ctx {
+  int device;
+};
+
+struct bmpc_plan {
+  bmpc_ctx* ctx;
+  HostPlan hp;
+  int batch;
+  Bundle* d_bundle = nullptr;
+  int32_t* d_tables = nullptr;
+  double* d_ws = nullptr;
+  bmpc_policy* d_pol = nullptr;
+  std::vector<bmpc_policy> h_pol;
+  double* d_in = nullptr;     // x | z | xref staging
+  double* d_out = nullptr;    // upred | xpred | bw | J staging
+  int32_t* d_iout = nullptr;  // status | iters
+  double* d_scratch = nullptr;
+  size_t scratch_len = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t user_stream = nullptr;
+  bool timing = false;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  double t_acc[2] = {0, 0};
+  int t_cnt = 0;
+};
+
+extern "C" {
+
+const char* bmpc_last_error(void) { return g_err.c_str(); }
+int bmpc_abi_version(void) { return BMPC_ABI_VERSION; }
+
+int bmpc_open(int hip_device, bmpc_ctx** out) {
+  if (!out) return fail(-22, "null output pointer");
+  int ndev = 0;
+  HIPCHECK(hipGetDeviceCount(&ndev));
+  if (hip_device < 0 || hip_device >= ndev) return fail(-19, "no such HIP device");
+  HIPCHECK(hipSetDevice(hip_device));
+  *out = new bmpc_ctx{hip_device};
+  return 0;
+}
+
+int bmpc_close(bmpc_ctx* ctx) {
+  delete ctx;
+  return 0;
+}
+
+int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_plan** out) {
+  if (!ctx || !desc || !out) return fail(-22, "null argument");
+  if (batch <= 0) return fail(-22, "batch must be positive");
+  HIPCHECK(hipSetDevice(ctx->device));
+  bmpc_plan* pl = new bmpc_plan();
+  pl->ctx = ctx;
+  pl->batch = batch;
+  std::string err = build_plan(*desc, pl->hp);
+  if (!err.empty()) {
+    delete pl;
+    return fail(-22, err);
+  }
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  auto cleanup = [&](int rc) {
+    bmpc_plan_destroy(pl);
+    return rc;
+  };
+  if (hipMalloc(&pl->d_tables, pl->hp.blob.size() * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&pl->d_bundle, sizeof(Bundle)) != hipSuccess ||
+      hipMalloc(&pl->d_ws, L.stride * (size_t)batch * sizeof(double)) != hipSuccess ||
+      hipMalloc(&pl->d_pol, sizeof(bmpc_policy) * (size_t)batch * P.m) != hipSuccess ||
+      hipMalloc(&pl->d_in, sizeof(double) * (size_t)batch * P.n * 3) != hipSuccess ||
+      hipMalloc(&pl->d_out, sizeof(double) * (size_t)batch * ((size_t)P.U * P.d + (size_t)P.T * P.n + P.nbranch + 1)) != hipSuccess ||
+      hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess)
+    return cleanup(fail(-12, "hipMalloc failed (out of device memory?)"));
+  if (hipMemcpy(pl->d_tables, pl->hp.blob.data(), pl->hp.blob.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(-5, "hipMemcpy tables failed"));
+  Bundle hb;
+  hb.P = P;
+  hb.L = L;
+  {
+    HostPlan tmp = pl->hp;       // re-point the table pointers at the device copy
+    tmp.point_tables(pl->d_tables);
+    hb.P.t = tmp.plan.t;
+  }
+  if (hipMemcpy(pl->d_bundle, &hb, sizeof(Bundle), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(pl->d_ws, 0, L.stride * (size_t)batch * sizeof(double)) != hipSuccess)
+    return cleanup(fail(-5, "plan upload failed"));
+  pl->h_pol.assign((size_t)batch * P.m, bmpc_policy{});
+  if (hipMemcpy(pl->d_pol, pl->h_pol.data(), sizeof(bmpc_policy) * pl->h_pol.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(-5, "policy upload failed"));
+  if (hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(-5, "hipStreamCreate failed"));
+  for (auto& e : pl->ev)
+    if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(-5, "hipEventCreate failed"));
+  *out = pl;
+  return 0;
+}
+
+int bmpc_plan_destroy(bmpc_plan* pl) {
+  if (!pl) return 0;
+  hipSetDevice(pl->ctx->device);
+  if (pl->stream) hipStreamSynchronize(pl->stream);
+  hipFree(pl->d_tables);
+  hipFree(pl->d_bundle);
+  hipFree(pl->d_ws);
+  hipFree(pl->d_pol);
+  hipFree(pl->d_in);
+  hipFree(pl->d_out);
+  hipFree(pl->d_iout);
+  hipFree(pl->d_scratch);
+  for (auto& e : pl->ev)
+    if (e) hipEventDestroy(e);
+  if (pl->stream) hipStreamDestroy(pl->stream);
+  delete pl;
+  return 0;
+}
+
+int bmpc_plan_info(const bmpc_plan* pl, int32_t* info) {
+  if (!pl || !info) return fail(-22, "null argument");
+  const Plan& P = pl->hp.plan;
+  info[BMPC_INFO_T] = P.T;
+  info[BMPC_INFO_U] = P.U;
+  info[BMPC_INFO_BDIM] = P.bdim;
+  info[BMPC_INFO_NBRANCH] = P.nbranch;
+  info[BMPC_INFO_NV] = P.nv;
+  info[BMPC_INFO_NEQ] = P.neq;
+  info[BMPC_INFO_NROWS] = P.nrows;
+  info[BMPC_INFO_NCONES] = P.ncones;
+  info[BMPC_INFO_LP] = P.nlp;
+  info[BMPC_INFO_BATCH] = pl->batch;
+  return 0;
+}
+
+int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask) {
+  if (!pl || !pol) return fail(-22, "null argument");
+  const int m = pl->hp.plan.m;
+  for (int e = 0; e < pl->batch; ++e)
+    if (!mask || mask[e])
+      memcpy(&pl->h_pol[(size_t)e * m], pol + (size_t)e * m, sizeof(bmpc_policy) * m);
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  HIPCHECK(hipMemcpyAsync(pl->d_pol, pl->h_pol.data(), sizeof(bmpc_policy) * pl->h_pol.size(),
+                          hipMemcpyHostToDevice, pl->stream));
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  return 0;
+}
+
+int bmpc_reset(bmpc_plan* pl, const uint8_t* mask) {
+  if (!pl) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  uint8_t* d_mask = nullptr;
+  if (mask) {
+    HIPCHECK(hipMalloc(&d_mask, pl->batch));
+    HIPCHECK(hipMemcpy(d_mask, mask, pl->batch, hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(k_reset, dim3((pl->batch + 255) / 256), dim3(256), 0, pl->stream, pl->d_ws,
+                     pl->hp.lay.stride, pl->hp.lay.misc, d_mask, pl->batch);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  if (d_mask) hipFree(d_mask);
+  return 0;
+}
+
+static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
+                        double* d_upred, double* d_xpred, double* d_bw, double* d_J,
+                        int32_t* d_status, int32_t* d_iters, hipStream_t s) {
+  const Plan& P = pl->hp.plan;
+  const int B = pl->batch;
+  if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[0], s));
+  if (P.desc.model == BMPC_MODEL_HIGHWAY)
+    hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_x, d_z, d_xref, B);
+  else
+    hipLaunchKernelGGL(k_tree<Quadruped>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_x, d_z, d_xref, B);
+  HIPCHECK(hipGetLastError());
+  if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[1], s));
+  if (P.desc.model == BMPC_MODEL_HIGHWAY)
+    hipLaunchKernelGGL(k_ipm<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+  else
+    hipLaunchKernelGGL(k_ipm<Quadruped>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+  HIPCHECK(hipGetLastError());
+  if (pl->timing) {
+    HIPCHECK(hipEventRecord(pl->ev[2], s));
+    HIPCHECK(hipEventSynchronize(pl->ev[2]));
+    float a = 0, b = 0;
+    HIPCHECK(hipEventElapsedTime(&a, pl->ev[0], pl->ev[1]));
+    HIPCHECK(hipEventElapsedTime(&b, pl->ev[1], pl->ev[2]));
+    pl->t_acc[0] += a;
+    pl->t_acc[1] += b;
+    pl->t_cnt += 1;
+  }
+  return 0;
+}
+
+int bmpc_solve(bmpc_plan* pl, const double* x, const double* z, const double* xref, double* upred,
+               double* xpred, double* branch_w, double* J, int32_t* status, int32_t* iters) {
+  if (!pl || !x || !z || !xref) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const size_t B = pl->batch, n = P.n;
+  hipStream_t s = pl->stream;
+  double* dx = pl->d_in;
+  double* dz = dx + B * n;
+  double* dr = dz + B * n;
+  HIPCHECK(hipMemcpyAsync(dx, x, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(dz, z, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(dr, xref, sizeof(double) * B * n, hipMemcpyHostToDevice, s));
+  double* up = pl->d_out;
+  double* xp = up + B * P.U * P.d;
+  double* bw = xp + B * P.T * P.n;
+  double* jj = bw + B * (P.nbranch - 1);
+  int32_t* st = pl->d_iout;
+  int32_t* it = st + B;
+  int rc = launch_solve(pl, dx, dz, dr, up, xp, bw, jj, st, it, s);
+  if (rc) return rc;
+  if (upred) HIPCHECK(hipMemcpyAsync(upred, up, sizeof(double) * B * P.U * P.d, hipMemcpyDeviceToHost, s));
+  if (xpred) HIPCHECK(hipMemcpyAsync(xpred, xp, sizeof(double) * B * P.T * P.n, hipMemcpyDeviceToHost, s));
+  if (branch_w) HIPCHECK(hipMemcpyAsync(branch_w, bw, sizeof(double) * B * (P.nbranch - 1), hipMemcpyDeviceToHost, s));
+  if (J) HIPCHECK(hipMemcpyAsync(J, jj, sizeof(double) * B, hipMemcpyDeviceToHost, s));
+  if (status) HIPCHECK(hipMemcpyAsync(status, st, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+  if (iters) HIPCHECK(hipMemcpyAsync(iters, it, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bmpc_solve_device(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
+                      double* d_upred, double* d_xpred, double* d_branch_w, double* d_J,
+                      int32_t* d_status, int32_t* d_iters, void* stream) {
+  if (!pl || !d_x || !d_z || !d_xref) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
+  return launch_solve(pl, d_x, d_z, d_xref, d_upred, d_xpred, d_branch_w, d_J, d_status, d_iters, s);
+}
+
+static int gather(bmpc_plan* pl, size_t off, int count, double* host) {
+  if (!host) return 0;
+  const size_t need = (size_t)pl->batch * count;
+  if (need > pl->scratch_len) {
+    hipFree(pl->d_scratch);
+    pl->d_scratch = nullptr;
+    HIPCHECK(hipMalloc(&pl->d_scratch, need * sizeof(double)));
+    pl->scratch_len = need;
+  }
+  hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, pl->stream, pl->d_ws, pl->hp.lay.stride, off,
+                     count, pl->d_scratch, pl->batch);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(host, pl->d_scratch, need * sizeof(double), hipMemcpyDeviceToHost, pl->stream));
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  return 0;
+}
+
+int bmpc_get_tree(bmpc_plan* pl, double* xbar, double* ubar, double* zbar, double* w, double* p,
+                  double* sol) {
+  if (!pl) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  int rc;
+  if ((rc = gather(pl, L.xbar, P.T * P.n, xbar))) return rc;
+  if ((rc = gather(pl, L.ubar, P.U * P.d, ubar))) return rc;
+  if ((rc = gather(pl, L.zbar, P.T * P.n, zbar))) return rc;
+  if ((rc = gather(pl, L.w, P.nbranch, w))) return rc;
+  if (P.bdim * P.m > 0 && (rc = gather(pl, L.p, P.bdim * P.m, p))) return rc;
+  if ((rc = gather(pl, L.sol, P.nv, sol))) return rc;
+  return 0;
+}
+
+int bmpc_enable_timing(bmpc_plan* pl, int on) {
+  if (!pl) return fail(-22, "null argument");
+  pl->timing = on != 0;
+  pl->t_acc[0] = pl->t_acc[1] = 0;
+  pl->t_cnt = 0;
+  return 0;
+}
+
+int bmpc_timing(bmpc_plan* pl, double* ms, int32_t* count) {
+  if (!pl) return fail(-22, "null argument");
+  const int c = pl->t_cnt;
+  if (ms) {
+    ms[0] = c ? pl->t_acc[0] / c : 0.0;
+    ms[1] = c ? pl->t_acc[1] / c : 0.0;
+  }
+  if (count) *count = c;
+  pl->t_acc[0] = pl->t_acc[1] = 0;
+  pl->t_cnt = 0;
+  return 0;
+}
+
+int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy* policies, int B,
+                    const double* x, const double* u, const double* z, double* A, double* Bm,
+                    double* C, double* xp, double* p, double* dp, double* zpred, double* h0,
+                    double* dh) {
+  if (!ctx || !desc || !policies || !x || !u || !z || B <= 0) return fail(-22, "null argument");
+  const int n = desc->n, d = desc->d, m = desc->m, N = desc->N;
+  if ((desc->model == BMPC_MODEL_HIGHWAY && (n != 4 || d != 2)) ||
+      (desc->model == BMPC_MODEL_QUADRUPED && (n != 3 || d != 3)) || m < 1 || m > BMPC_MAX_M || N < 1)
+    return fail(-22, "bad model dimensions");
+  HIPCHECK(hipSetDevice(ctx->device));
+  const size_t sizes[] = {(size_t)n * n, (size_t)n * d, (size_t)n, (size_t)n, (size_t)m,
+                          (size_t)m * n, (size_t)N * m * n, 1, (size_t)n};
+  double* hosts[] = {A, Bm, C, xp, p, dp, zpred, h0, dh};
+  size_t tot = (size_t)B * (2 * n + d);
+  for (size_t s : sizes) tot += (size_t)B * s;
+  double* buf = nullptr;
+  bmpc_policy* dpol = nullptr;
+  HIPCHECK(hipMalloc(&buf, tot * sizeof(double)));
+  HIPCHECK(hipMalloc(&dpol, sizeof(bmpc_policy) * (size_t)B * m));
+  HIPCHECK(hipMemcpy(dpol, policies, sizeof(bmpc_policy) * (size_t)B * m, hipMemcpyHostToDevice));
+  double* dxp = buf;
+  double* dup = dxp + (size_t)B * n;
+  double* dzp = dup + (size_t)B * d;
+  HIPCHECK(hipMemcpy(dxp, x, sizeof(double) * B * n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dup, u, sizeof(double) * B * d, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dzp, z, sizeof(double) * B * n, hipMemcpyHostToDevice));
+  double* dev[9];
+  double* cur = dzp + (size_t)B * n;
+  for (int i = 0; i < 9; ++i) {
+    dev[i] = hosts[i] ? cur : nullptr;
+    cur += (size_t)B * sizes[i];
+  }
+  if (dp && !p) dev[5] = nullptr;
+  if (dh && !h0) dev[8] = nullptr;
+  if (desc->model == BMPC_MODEL_HIGHWAY)
+    hipLaunchKernelGGL(k_model<Highway>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+  else
+    hipLaunchKernelGGL(k_model<Quadruped>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipDeviceSynchronize());
+  for (int i = 0; i < 9; ++i)
+    if (hosts[i] && dev[i]) HIPCHECK(hipMemcpy(hosts[i], dev[i], sizeof(double) * B * sizes[i], hipMemcpyDeviceToHost));
+  hipFree(buf);
+  hipFree(dpol);
+  return 0;
+}
+
+}  // extern "C"

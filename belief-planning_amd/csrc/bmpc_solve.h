@@ -1,0 +1,91 @@
+// bmpc_solve.h -- one controller solve of one ego: tree update -> IPM -> unpack.
+//
+// BranchMPC_CVaR.solve (MPC_branch.py:2043-2092): xRef update, inittree/updatetree,
+// (re)assembly, ecos.solve, unpackSolution (:2096-2106) with the "keep the previous
+// solution when infeasible" rule, OldInput = uPred[0].
+#pragma once
+
+#include "bmpc_ipm.h"
+
+namespace bmpc {
+
+// phase 2: IPM + unpack (reads the tree written by tree_update; xref copied there)
+template <class X, class M>
+BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, EgoView E) {
+  constexpr int NX = M::NX, NU = M::NU;
+  double* ws = E.ws;
+  const bool init = ws[L.misc + MISC_INIT] != 0.0;
+  const double* xref = ws + L.xref;
+  Ctx C;
+  C.P = &P;
+  C.L = &L;
+  C.ws = ws;
+  C.ralpha = P.desc.ralpha;
+  for (int c = 0; c < NX; ++c) {
+    double v = 0.0;
+    for (int r = 0; r < NX; ++r) v += xref[r] * P.desc.Q[r * NX + c];
+    C.qx[c] = v;
+  }
+  if (!init) {   // first solve freezes Jcons = xRef Q xRef (MPC_branch.py:1939)
+    double j = 0.0;
+    for (int c = 0; c < NX; ++c) j += C.qx[c] * xref[c];
+    C.jcons = j;
+  } else {
+    C.jcons = ws[L.misc + MISC_JCONS];
+  }
+  ex.sync();
+  IpmResult r = ipm_solve<X, NX, NU>(ex, C);
+  // ---- unpack -----------------------------------------------------------------------------
+  const double* sol = ws + L.sol;
+  const bool feasible = r.exit_flag >= 0;
+  if (feasible) {
+    for (int i = ex.lane; i < P.U * NU; i += ex.nlanes) {
+      const double v = sol[P.oU + i];
+      ws[L.upred + i] = v;
+      ws[L.uLin + i] = v;
+    }
+    for (int i = ex.lane; i < NU; i += ex.nlanes) ws[L.uLin + P.U * NU + i] = sol[P.oU + (P.U - 1) * NU + i];
+    for (int i = ex.lane; i < P.T * NX; i += ex.nlanes) ws[L.xpred + i] = sol[P.oX + i];
+  }
+  for (int i = ex.lane; i < P.bdim * P.m; i += ex.nlanes) ws[L.pprev + i] = ws[L.p + i];
+  ex.sync();
+  if (ex.lane == 0) {
+    ws[L.misc + MISC_INIT] = 1.0;
+    ws[L.misc + MISC_JCONS] = C.jcons;
+    for (int i = 0; i < NU; ++i) ws[L.misc + MISC_OLDU + i] = ws[L.upred + i];
+  }
+  ex.sync();
+  return r;
+}
+
+template <class X, class M>
+BMPC_HD IpmResult solve_ego(const X& ex, const Plan& P, const Layout& L, EgoView E,
+                            const double* x, const double* z, const double* xref) {
+  tree_update<X, M>(ex, P, L, E, x, z, xref);
+  return solve_ego_ipm<X, M>(ex, P, L, E);
+}
+
+// bmpc_model_eval for one point
+template <class M>
+BMPC_HD void model_eval_point(const bmpc_plan_desc& D, const bmpc_policy* pol, const double* x,
+                              const double* u, const double* z, double* A, double* Bm, double* C,
+                              double* xp, double* p, double* dp, double* zpred, double* h0,
+                              double* dh) {
+  constexpr int NX = M::NX, NU = M::NU;
+  double tA[NX * NX], tB[NX * NU], tC[NX], txp[NX];
+  linearize<M>(D.dt, x, u, tA, tB, tC, txp);
+  if (A)
+    for (int i = 0; i < NX * NX; ++i) A[i] = tA[i];
+  if (Bm)
+    for (int i = 0; i < NX * NU; ++i) Bm[i] = tB[i];
+  if (C)
+    for (int i = 0; i < NX; ++i) C[i] = tC[i];
+  if (xp)
+    for (int i = 0; i < NX; ++i) xp[i] = txp[i];
+  if (p) branch_eval<M>(D.mc, D.dt, D.N, D.m, pol, x, z, p, dp);
+  if (zpred)
+    for (int i = 0; i < D.m; ++i) rollout<M>(D.dt, D.N, pol[i], z, zpred + i * NX, D.m * NX);
+  if (h0) col_eval<M>(D.mc, x, z, h0, dh);
+}
+
+}  // namespace bmpc

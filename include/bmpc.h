@@ -1,0 +1,182 @@
+/*
+ * bmpc.h -- C ABI of the MI355X batched branch-MPC library (libbmpc.so).
+ *
+ * Drop-in boundary for the reference's controller / predictive-model surface
+ * (Gavinli-lgf/belief-planning).  Every entry point replaces a reference interface:
+ *
+ *   bmpc_plan_create   <- BranchMPC_CVaR.__init__      MPC_branch.py:1601-1669
+ *                         BranchMPCProx.__init__        MPC_branch.py:84-128
+ *                         Init_MPC.initBranchMPC/initquadBranchMPC  Init_MPC.py:40-94
+ *                         PredictiveModel.__init__      highway_branch_dyn.py:264-281,
+ *                                                       quadruped_branch_dyn.py:155-173
+ *   bmpc_set_policies  <- PredictiveModel.update_backup highway_branch_dyn.py:331-334
+ *                         (the backup lambdas, traced to descriptors)
+ *   bmpc_reset         <- "self.BT is None" first-solve path (inittree) MPC_branch.py:2062-2064
+ *   bmpc_solve         <- BranchMPC_CVaR.solve           MPC_branch.py:2043-2092
+ *                         BranchMPCProx.solve             MPC_branch.py:384-423
+ *                         (tree update, linearisation, assembly, ecos.solve / OSQP, unpack)
+ *   bmpc_get_tree      <- BranchTree fields + BT2array    MPC_branch.py:65-78,2108-2122
+ *   bmpc_model_eval    <- PredictiveModel.dyn_linearization / branch_eval / zpred_eval /
+ *                         col_eval                         highway_branch_dyn.py:284-325
+ *
+ * Conventions: all host buffers are caller-owned, C-contiguous, ego-major, float64
+ * (int32 for status/iteration counts).  Return codes are 0 on success and a negative
+ * errno-style code on failure; bmpc_last_error() gives a thread-local message.  A plan
+ * owns its device buffers and the per-ego persistent warm-start state; calls are
+ * synchronous on the plan's HIP stream unless the *_device variant is used.
+ * Per-ego status follows ECOS exit codes for the CVaR controller (>= 0 means
+ * "feasible", MPC_branch.py:2141) and OSQP status_val for the QP controllers
+ * (1 means "feasible", MPC_branch.py:482).
+ */
+#ifndef BMPC_H
+#define BMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BMPC_ABI_VERSION 1
+
+#define BMPC_MAX_N 8      /* state dimension            */
+#define BMPC_MAX_D 4      /* input dimension            */
+#define BMPC_MAX_FX 8     /* rows of Fx                 */
+#define BMPC_MAX_FU 8     /* rows of Fu                 */
+#define BMPC_MAX_M 4      /* backup policies per branch */
+
+/* controller kinds */
+enum {
+  BMPC_CTRL_CVAR = 0, /* BranchMPC_CVaR  (ECOS SOCP)   MPC_branch.py:1598 */
+  BMPC_CTRL_PROX = 1  /* BranchMPCProx   (OSQP QP)     MPC_branch.py:82   */
+};
+
+/* predictive models */
+enum {
+  BMPC_MODEL_HIGHWAY = 0,   /* highway_branch_dyn.PredictiveModel   */
+  BMPC_MODEL_QUADRUPED = 1  /* quadruped_branch_dyn.PredictiveModel */
+};
+
+/* backup-policy kinds (what the traced lambdas lower to) */
+enum {
+  BMPC_POL_MAINTAIN = 0,        /* backup_maintain(x,cons)          p = {Kpsi}          */
+  BMPC_POL_BRAKE = 1,           /* backup_brake(x,cons)             p = {Kpsi}          */
+  BMPC_POL_LC = 2,              /* backup_lc(x,x0)                  p = x0[0..3]        */
+  BMPC_POL_MAINTAIN_TRACKV = 3, /* backup_maintain_trackV(x,cons,v0) p = {Kpsi, v0}     */
+  BMPC_POL_FORWARD = 4,         /* quadruped backup_forward(x,v0)   p = {v0}            */
+  BMPC_POL_STOP = 5             /* quadruped backup_stop(x)                             */
+};
+
+typedef struct {
+  int32_t kind;
+  int32_t reserved;
+  double p[4];
+} bmpc_policy;
+
+/* POD description of one controller + predictive model (one plan = one batch of egos
+ * that share it).  Matrices are row-major with the leading dimension equal to their
+ * logical size (Q is n*n, Fx is nFx*n, Fu is nFu*d, ...). */
+typedef struct {
+  int32_t controller;   /* BMPC_CTRL_*                                   */
+  int32_t model;        /* BMPC_MODEL_*                                  */
+  int32_t n, d;         /* state / input dimension                      */
+  int32_t N, NB, m;     /* steps per branch, branching depth, policies  */
+  int32_t nFx, nFu;     /* rows of Fx, Fu                                */
+  int32_t maxit;        /* IPM iterations (ECOS default 100)            */
+  double dt;
+  double ralpha;        /* CVaR alpha (BranchMPC_CVaR ralpha)            */
+  double Q[BMPC_MAX_N * BMPC_MAX_N];
+  double R[BMPC_MAX_D * BMPC_MAX_D];
+  double Qf[BMPC_MAX_N * BMPC_MAX_N];
+  double dR[BMPC_MAX_D];
+  double Fx[BMPC_MAX_FX * BMPC_MAX_N];
+  double bx[BMPC_MAX_FX];
+  double Fu[BMPC_MAX_FU * BMPC_MAX_D];
+  double bu[BMPC_MAX_FU];
+  double Qslack[2];
+  /* model constants:
+   *   highway   {L, W, s1, N_lane}          (Branch_constants + PredictiveModel ctor)
+   *   quadruped {L1, W1, L2, W2, col_tol, s1} (Quad_constants)                       */
+  double mc[8];
+  double feastol, abstol, reltol; /* ECOS tolerances (defaults 1e-8)              */
+} bmpc_plan_desc;
+
+typedef struct bmpc_ctx bmpc_ctx;
+typedef struct bmpc_plan bmpc_plan;
+
+/* plan geometry returned by bmpc_plan_info (all int32) */
+enum {
+  BMPC_INFO_T = 0,      /* totalx  (state nodes)                 */
+  BMPC_INFO_U,          /* totalu  (input nodes)                 */
+  BMPC_INFO_BDIM,       /* non-leaf branches                     */
+  BMPC_INFO_NBRANCH,    /* branches incl. root                   */
+  BMPC_INFO_NV,         /* primal variables of the solver vector */
+  BMPC_INFO_NEQ,        /* equality rows                         */
+  BMPC_INFO_NROWS,      /* conic rows (LP + SOC)                 */
+  BMPC_INFO_NCONES,     /* second-order cones                    */
+  BMPC_INFO_LP,         /* LP rows (dims['l'])                   */
+  BMPC_INFO_BATCH,
+  BMPC_INFO_COUNT
+};
+
+const char* bmpc_last_error(void);
+int bmpc_abi_version(void);
+
+int bmpc_open(int hip_device, bmpc_ctx** out);
+int bmpc_close(bmpc_ctx* ctx);
+
+int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_plan** out);
+int bmpc_plan_destroy(bmpc_plan* plan);
+int bmpc_plan_info(const bmpc_plan* plan, int32_t* info /* [BMPC_INFO_COUNT] */);
+
+/* update_backup: policies[batch][m]; mask[batch] (NULL = all egos) */
+int bmpc_set_policies(bmpc_plan* plan, const bmpc_policy* policies, const uint8_t* mask);
+/* forget the warm start (next solve runs inittree); mask NULL = all egos */
+int bmpc_reset(bmpc_plan* plan, const uint8_t* mask);
+
+/* One controller solve for every ego of the plan (host buffers).
+ *   x, z, xref : [batch][n]
+ *   upred      : [batch][U][d]     xpred : [batch][T][n]
+ *   branch_w   : [batch][nbranch-1] (BFS order of BT2array)
+ *   J          : [batch]            objective (CVaR: the J variable; QP: cost)
+ *   status     : [batch]            ECOS exitFlag / OSQP status_val
+ *   iters      : [batch]
+ * Any output pointer may be NULL. */
+int bmpc_solve(bmpc_plan* plan, const double* x, const double* z, const double* xref,
+               double* upred, double* xpred, double* branch_w, double* J,
+               int32_t* status, int32_t* iters);
+
+/* Same with device pointers, enqueued on `stream` (hipStream_t, NULL = plan stream),
+ * no host synchronisation. */
+int bmpc_solve_device(bmpc_plan* plan, const double* d_x, const double* d_z,
+                      const double* d_xref, double* d_upred, double* d_xpred,
+                      double* d_branch_w, double* d_J, int32_t* d_status,
+                      int32_t* d_iters, void* stream);
+
+/* Tree of the last solve (host copies; NULL skips):
+ *   xbar,zbar [batch][T][n]  ubar [batch][U][d]  w [batch][nbranch]
+ *   p [batch][bdim][m]       sol [batch][nv]   (full primal vector, reference layout) */
+int bmpc_get_tree(bmpc_plan* plan, double* xbar, double* ubar, double* zbar, double* w,
+                  double* p, double* sol);
+
+/* Average device time per call of each kernel over the solves since the last call
+ * (HIP events on the launch stream); ms[0] = tree/linearisation kernel, ms[1] = IPM
+ * kernel, count = number of solves timed.  Timing must be enabled first. */
+int bmpc_enable_timing(bmpc_plan* plan, int on);
+int bmpc_timing(bmpc_plan* plan, double* ms /* [2] */, int32_t* count);
+
+/* Batched model evaluation at B independent points (parity entry for the model
+ * functions).  policies [B][m].  Outputs (NULL skips):
+ *   A [B][n][n], Bm [B][n][d], C [B][n], xp [B][n]    at (x, u)
+ *   p [B][m], dp [B][m][n]                            branch_eval(x, z)
+ *   zpred [B][N][m*n]                                 zpred_eval(z)
+ *   h0 [B], dh [B][n]                                 col_eval(x, z) */
+int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy* policies,
+                    int B, const double* x, const double* u, const double* z,
+                    double* A, double* Bm, double* C, double* xp, double* p, double* dp,
+                    double* zpred, double* h0, double* dh);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BMPC_H */

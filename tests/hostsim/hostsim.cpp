@@ -1,0 +1,143 @@
+// hostsim.cpp -- TEST-ONLY host build of the GPU solver templates.
+//
+// Instantiates the wave-cooperative templates of belief-planning_amd/csrc with a 1-lane
+// host executor so the CPU test suite can check the kernel *algorithm* against the oracle
+// without a GPU.  It exports its own `hs_*` symbols (never the product C ABI) and is never
+// loaded by the belief-planning_amd package: the product path is libbmpc.so (HIP) only.
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "bmpc_plan.h"
+#include "bmpc_solve.h"
+
+using namespace bmpc;
+
+namespace {
+struct HostExec {
+  int lane = 0;
+  int nlanes = 1;
+  void sync() const {}
+  double sum(double v) const { return v; }
+  double max(double v) const { return v; }
+  double min(double v) const { return v; }
+};
+
+struct HS {
+  HostPlan hp;
+  int batch;
+  std::vector<double> ws;
+  std::vector<bmpc_policy> pol;
+};
+thread_local std::string g_err;
+}  // namespace
+
+extern "C" {
+
+const char* hs_last_error(void) { return g_err.c_str(); }
+
+int hs_create(const bmpc_plan_desc* desc, int batch, void** out) {
+  HS* h = new HS();
+  g_err = build_plan(*desc, h->hp);
+  if (!g_err.empty()) {
+    delete h;
+    return -22;
+  }
+  h->batch = batch;
+  h->ws.assign(h->hp.lay.stride * (size_t)batch, 0.0);
+  h->pol.assign((size_t)batch * desc->m, bmpc_policy{});
+  *out = h;
+  return 0;
+}
+
+int hs_destroy(void* p) {
+  delete (HS*)p;
+  return 0;
+}
+
+int hs_info(void* p, int32_t* info) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  info[BMPC_INFO_T] = P.T;
+  info[BMPC_INFO_U] = P.U;
+  info[BMPC_INFO_BDIM] = P.bdim;
+  info[BMPC_INFO_NBRANCH] = P.nbranch;
+  info[BMPC_INFO_NV] = P.nv;
+  info[BMPC_INFO_NEQ] = P.neq;
+  info[BMPC_INFO_NROWS] = P.nrows;
+  info[BMPC_INFO_NCONES] = P.ncones;
+  info[BMPC_INFO_LP] = P.nlp;
+  info[BMPC_INFO_BATCH] = h->batch;
+  return 0;
+}
+
+int hs_set_policies(void* p, const bmpc_policy* pol) {
+  HS* h = (HS*)p;
+  memcpy(h->pol.data(), pol, sizeof(bmpc_policy) * h->pol.size());
+  return 0;
+}
+
+int hs_solve(void* p, const double* x, const double* z, const double* xref, double* upred,
+             double* xpred, double* bw, double* J, int32_t* status, int32_t* iters) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  HostExec ex;
+  for (int e = 0; e < h->batch; ++e) {
+    EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
+    IpmResult r;
+    if (P.desc.model == BMPC_MODEL_HIGHWAY)
+      r = solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+    else
+      r = solve_ego<HostExec, Quadruped>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+    const double* ws = E.ws;
+    if (upred) memcpy(upred + (size_t)e * P.U * P.d, ws + L.upred, sizeof(double) * P.U * P.d);
+    if (xpred) memcpy(xpred + (size_t)e * P.T * P.n, ws + L.xpred, sizeof(double) * P.T * P.n);
+    if (bw) memcpy(bw + (size_t)e * (P.nbranch - 1), ws + L.w + 1, sizeof(double) * (P.nbranch - 1));
+    if (J) J[e] = ws[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+  return 0;
+}
+
+int hs_get_tree(void* p, double* xbar, double* ubar, double* zbar, double* w, double* pr,
+                double* sol) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  for (int e = 0; e < h->batch; ++e) {
+    const double* ws = h->ws.data() + L.stride * e;
+    if (xbar) memcpy(xbar + (size_t)e * P.T * P.n, ws + L.xbar, sizeof(double) * P.T * P.n);
+    if (zbar) memcpy(zbar + (size_t)e * P.T * P.n, ws + L.zbar, sizeof(double) * P.T * P.n);
+    if (ubar) memcpy(ubar + (size_t)e * P.U * P.d, ws + L.ubar, sizeof(double) * P.U * P.d);
+    if (w) memcpy(w + (size_t)e * P.nbranch, ws + L.w, sizeof(double) * P.nbranch);
+    if (pr) memcpy(pr + (size_t)e * P.bdim * P.m, ws + L.p, sizeof(double) * P.bdim * P.m);
+    if (sol) memcpy(sol + (size_t)e * P.nv, ws + L.sol, sizeof(double) * P.nv);
+  }
+  return 0;
+}
+
+int hs_model_eval(const bmpc_plan_desc* D, const bmpc_policy* pol, int B, const double* x,
+                  const double* u, const double* z, double* A, double* Bm, double* C, double* xp,
+                  double* p, double* dp, double* zpred, double* h0, double* dh) {
+  const int n = D->n, d = D->d, m = D->m, N = D->N;
+  for (int b = 0; b < B; ++b) {
+    const bmpc_policy* pb = pol + (size_t)b * m;
+#define OFF(ptr, k) (ptr ? ptr + (size_t)b * (k) : nullptr)
+    if (D->model == BMPC_MODEL_HIGHWAY)
+      model_eval_point<Highway>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n), OFF(zpred, N * m * n),
+                                OFF(h0, 1), OFF(dh, n));
+    else
+      model_eval_point<Quadruped>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                  OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),
+                                  OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n));
+#undef OFF
+  }
+  return 0;
+}
+
+}  // extern "C"

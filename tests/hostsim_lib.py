@@ -1,0 +1,106 @@
+"""ctypes wrapper of the TEST-ONLY host build (tests/hostsim/libbmpc_hostsim.so).
+
+Builds the shared object on first use with g++ from the same csrc templates the HIP
+kernels instantiate, so CPU tests can check the kernel algorithm against the oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+PKG = os.path.join(REPO, "belief-planning_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+from bmpc import abi  # noqa: E402
+
+SO = os.path.join(HERE, "hostsim", "libbmpc_hostsim.so")
+SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", "bmpc_plan.cpp")]
+HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")]
+
+
+def build(force=False):
+    newest = max(os.path.getmtime(p) for p in SRCS + HDRS + [os.path.join(REPO, "include", "bmpc.h")])
+    if force or not os.path.exists(SO) or os.path.getmtime(SO) < newest:
+        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas",
+               "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", SO]
+        subprocess.check_call(cmd)
+    return SO
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        _lib.hs_last_error.restype = C.c_char_p
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class HostSim:
+    def __init__(self, desc, batch):
+        self.desc = desc
+        self.batch = batch
+        h = C.c_void_p()
+        rc = lib().hs_create(C.byref(desc), batch, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(lib().hs_last_error().decode())
+        self.h = h
+        info = np.zeros(abi.INFO_COUNT, np.int32)
+        lib().hs_info(h, _p(info))
+        self.T, self.U, self.bdim, self.nbranch, self.nv = (int(info[i]) for i in range(5))
+        self.info = info
+
+    def __del__(self):
+        try:
+            lib().hs_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_policies(self, pol_rows):
+        arr = abi.policy_array(pol_rows)
+        lib().hs_set_policies(self.h, arr)
+
+    def solve(self, x, z, xref):
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        x, z, xref = (np.ascontiguousarray(np.asarray(v, float).reshape(B, n)) for v in (x, z, xref))
+        up = np.zeros((B, self.U, d))
+        xp = np.zeros((B, self.T, n))
+        bw = np.zeros((B, self.nbranch - 1))
+        J = np.zeros(B)
+        st = np.zeros(B, np.int32)
+        it = np.zeros(B, np.int32)
+        lib().hs_solve(self.h, _p(x), _p(z), _p(xref), _p(up), _p(xp), _p(bw), _p(J), _p(st), _p(it))
+        return dict(upred=up, xpred=xp, branch_w=bw, J=J, status=st, iters=it)
+
+    def tree(self):
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),
+                   zbar=np.zeros((B, self.T, n)), w=np.zeros((B, self.nbranch)),
+                   p=np.zeros((B, self.bdim, self.desc.m)), sol=np.zeros((B, self.nv)))
+        lib().hs_get_tree(self.h, *(_p(out[k]) for k in ("xbar", "ubar", "zbar", "w", "p", "sol")))
+        return out
+
+
+def model_eval(desc, pol_rows, x, u, z):
+    x, u, z = (np.ascontiguousarray(np.atleast_2d(np.asarray(v, float))) for v in (x, u, z))
+    B, n, d, m, N = x.shape[0], desc.n, desc.d, desc.m, desc.N
+    out = dict(A=np.zeros((B, n, n)), B=np.zeros((B, n, d)), C=np.zeros((B, n)), xp=np.zeros((B, n)),
+               p=np.zeros((B, m)), dp=np.zeros((B, m, n)), zpred=np.zeros((B, N, m * n)),
+               h0=np.zeros(B), dh=np.zeros((B, n)))
+    arr = abi.policy_array(pol_rows)
+    lib().hs_model_eval(C.byref(desc), arr, B, _p(x), _p(u), _p(z),
+                        *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")))
+    return out

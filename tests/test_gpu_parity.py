@@ -1,0 +1,126 @@
+"""GPU parity tests: libbmpc.so (gfx950 kernels, through the C ABI) vs the oracle.
+
+Tolerances (stated per check):
+* model functions: 1e-12 relative -- same closed-form expressions, fp64;
+* solver: the reference solves with ECOS to feastol=abstol=reltol=1e-8 (MPC_branch.py:2136),
+  so a solution is only defined to that precision.  J must agree to 1e-6 relative and the
+  applied input uPred[0] to 1e-4 absolute (|u| <= 6); the unique part of the primal vector
+  (everything except the cost-free leaf-terminal slacks) to 1e-3 absolute.  GPU vs the
+  host build of the same algorithm is compared tighter (J 1e-7 rel, uPred 1e-5 abs).
+"""
+import numpy as np
+import pytest
+
+from common import (cone_problem, golden, highway_desc, highway_desc_from_golden, highway_policy_rows,
+                    seeded_batch, unique_mask)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from bmpc import plan
+    plan.context(0)
+    return plan
+
+
+def test_library_is_native(gpu):
+    from bmpc import _lib
+    assert _lib.lib().bmpc_abi_version() == 1
+
+
+def test_model_eval_matches_oracle(gpu):
+    from oracle.model import HighwayModel, highway_policies
+    rng = np.random.default_rng(3)
+    B = 256
+    desc = highway_desc(N=20, NB=1)
+    x = np.stack([rng.uniform(-5, 5, B), rng.uniform(0, 13, B), rng.uniform(10, 30, B), rng.normal(0, .1, B)], 1)
+    u = np.stack([rng.uniform(-6, 6, B), rng.uniform(-.3, .3, B)], 1)
+    z = x + np.stack([rng.uniform(-10, 30, B), rng.uniform(-6, 6, B), rng.uniform(-5, 5, B), np.zeros(B)], 1)
+    tg = np.stack([np.zeros(B), rng.choice([1.8, 5.4, 9.0], B), np.full(B, 20.0), np.zeros(B)], 1)
+    out = gpu.model_eval(desc, highway_policy_rows(tg), x, u, z)
+    for b in range(0, B, 17):
+        mdl = HighwayModel(20, 0.1, highway_policies(0.1, tg[b]))
+        A, Bm, C, xp = mdl.dyn_linearization(x[b], u[b])
+        p, dp = mdl.branch_eval(x[b], z[b])
+        h0, dh = mdl.col_eval(x[b], z[b])
+        zp = mdl.zpred_eval(z[b])
+        for got, ref in ((out["A"][b], A), (out["B"][b], Bm), (out["C"][b], C), (out["xp"][b], xp),
+                         (out["p"][b], p), (out["dp"][b], dp), (out["zpred"][b], zp),
+                         (out["h0"][b], h0), (out["dh"][b], dh)):
+            np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["highway_n20_nb1", "highway_n8_nb2"])
+def test_closed_loop_matches_golden(gpu, name):
+    """Replay the reference's closed loop (inputs recorded from the reference controller
+    under stubs) through one GPU ego; compare with the recorded solutions."""
+    g = golden(name)
+    desc = highway_desc_from_golden(g)
+    pl = gpu.BatchPlan(desc, 1)
+    steps = min(len(g["traj_x"]), 20)
+    keep = set(int(v) for v in g["keep"])
+    mask = unique_mask(pl.T, int(g["NB"]), int(g["N"]), 3)
+    for t in range(steps):
+        pl.set_policies(highway_policy_rows(g["traj_lc_target"][t]))
+        r = pl.solve(g["traj_x"][t][None], g["traj_z"][t][None], g["traj_xRef"][t][None])
+        assert r["status"][0] >= 0, (t, r["status"][0])
+        Jref = g["traj_J"][t]
+        assert abs(r["J"][0] - Jref) <= 1e-6 * max(1.0, abs(Jref)), (t, r["J"][0], Jref)
+        np.testing.assert_allclose(r["upred"][0, 0], g["traj_u"][t], atol=1e-4)
+        if t in keep:
+            sol = pl.tree()["sol"][0]
+            ref = g[f"s{t}_sol"]
+            scale = np.maximum(1.0, np.abs(ref))
+            err = np.abs(sol - ref)[mask] / scale[mask]
+            assert err.max() < 1e-3, (t, err.max())
+
+
+def test_batch_matches_host_build(gpu):
+    """Seeded batch: every GPU ego equals the host build of the same algorithm."""
+    import hostsim_lib as H
+    B = 64
+    x, z, xref, tgt = seeded_batch(B, seed=1)
+    desc = highway_desc(N=20, NB=1)
+    pl = gpu.BatchPlan(desc, B)
+    pl.set_policies(highway_policy_rows(tgt))
+    hs = H.HostSim(desc, B)
+    hs.set_policies(highway_policy_rows(tgt))
+    for step in range(3):
+        r = pl.solve(x, z, xref)
+        h = hs.solve(x, z, xref)
+        np.testing.assert_array_equal(r["status"] >= 0, h["status"] >= 0)
+        ok = h["status"] >= 0
+        np.testing.assert_allclose(r["J"][ok], h["J"][ok], rtol=1e-7)
+        np.testing.assert_allclose(r["upred"][ok], h["upred"][ok], atol=1e-5)
+        u0 = r["upred"][:, 0]
+        x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
+        z = z + 0.1 * np.stack([z[:, 2] * np.cos(z[:, 3]), z[:, 2] * np.sin(z[:, 3]), 0 * z[:, 0], 0 * z[:, 0]], 1)
+
+
+def test_full_batch_certified(gpu):
+    """B=4096 (the metric batch): every ego returns a feasible ECOS-class status and a
+    finite plan; a sample is re-solved by the CPU oracle and must agree on J."""
+    from oracle.ecos_ipm import ecos_solve
+    from oracle.model import HighwayModel, highway_policies
+    from oracle.tree import CVaRController
+    B = 4096
+    x, z, xref, tgt = seeded_batch(B, seed=0)
+    desc = highway_desc(N=20, NB=1)
+    pl = gpu.BatchPlan(desc, B)
+    pl.set_policies(highway_policy_rows(tgt))
+    r = pl.solve(x, z, xref)
+    assert np.all(r["status"] >= 0), np.unique(r["status"], return_counts=True)
+    assert np.all(np.isfinite(r["J"])) and np.all(np.isfinite(r["upred"]))
+    Fx = np.array([[0., 1, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1], [0, 0, 0, -1]])
+    for e in (0, 1, 777, 4095):
+        mdl = HighwayModel(20, 0.1, highway_policies(0.1, tgt[e]))
+        c = CVaRController(mdl, 20, 1, np.diag([0., 3, 3, 10]), np.diag([1., 100]), Fx,
+                           [4 * 3.6 - 1.25, -1.25, .25, .25], np.kron(np.eye(2), [1, -1]).T,
+                           [6., 6., .3, .3], [0, 300], xref[e], 0.9, solver=ecos_solve)
+        c.solve(x[e], z[e], xref[e])
+        assert abs(r["J"][e] - c.last_info["x"][-1]) <= 1e-6 * max(1, abs(r["J"][e]))
+        np.testing.assert_allclose(r["upred"][e, 0], c.uPred[0], atol=1e-4)

@@ -1,0 +1,264 @@
+"""Generate golden fixtures from the reference's own controller code (run HERE only).
+
+The reference's ``MPC_branch`` / ``Init_MPC`` / ``utils`` import fine once the three
+solver packages they name are replaced by import stubs (SURVEY §8c route 1):
+
+* ``cvxopt`` -- only ``solvers.options`` is touched (``MPC_branch.py:3,15``);
+* ``ecos``   -- ``ecos.solve`` is replaced by a recorder that captures the exact
+  ``(c, G, h, dims, A, b)`` the reference assembles and answers with the oracle's
+  ECOS-algorithm restatement (``oracle/ecos_ipm.py``);
+* ``osqp``   -- likewise for ``OSQP.setup/solve`` (quadruped ``BranchMPCProx``).
+
+The predictive model handed to the reference controller is the oracle's NumPy
+restatement of the CasADi graphs (CasADi is absent).  So the *tree bookkeeping, warm
+start, linearisation schedule and problem assembly* in the fixtures are produced by the
+reference code itself; model values come from the oracle; solutions from the oracle IPM.
+
+Outputs ``tests/golden/*.npz`` (data only, no reference source).  Usage:
+    python tools/gen_golden.py [--quick]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import scipy.sparse as sp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from oracle import ecos_ipm, qp_ipm  # noqa: E402
+from oracle.env import HighwayOvertake  # noqa: E402
+from oracle.model import HighwayModel, QuadrupedModel, highway_policies, quadruped_policies  # noqa: E402
+from oracle.tree import ConeProblem, QPProblem  # noqa: E402
+
+CURRENT = {}
+
+
+def install_stubs():
+    cv = types.ModuleType("cvxopt")
+    cvs = types.ModuleType("cvxopt.solvers")
+    cvs.options = {}
+    cvs.qp = None
+    cv.solvers, cv.spmatrix, cv.matrix = cvs, None, None
+    sys.modules["cvxopt"], sys.modules["cvxopt.solvers"] = cv, cvs
+
+    ec = types.ModuleType("ecos")
+
+    def ecos_solve(c, G, h, dims, A=None, b=None, **kw):
+        mpc = CURRENT["mpc"]
+        prob = ConeProblem(np.array(c, float), sp.csc_matrix(G, copy=True), np.array(h, float),
+                           {"l": int(dims["l"]), "q": [int(v) for v in dims["q"]]},
+                           sp.csc_matrix(A, copy=True), np.array(b, float), ref_cone_boost(mpc))
+        x, info = ecos_ipm.ecos_solve(prob)
+        CURRENT["captured"] = (prob, x, info, kw)
+        return {"x": x, "y": info["y"], "z": info["z"], "s": info["s"],
+                "info": {"exitFlag": info["exitFlag"], "iter": info["iter"]}}
+
+    ec.solve = ecos_solve
+    sys.modules["ecos"] = ec
+
+    oq = types.ModuleType("osqp")
+
+    class OSQP:
+        def setup(self, P, q, A, l, u, **kw):
+            self.prob = QPProblem(sp.csc_matrix(P, copy=True), np.array(q, float), sp.csc_matrix(A, copy=True),
+                                  np.array(l, float), np.array(u, float),
+                                  int(np.sum(~np.isfinite(l))))
+            self.kw = kw
+
+        def warm_start(self, **kw):
+            pass
+
+        def solve(self):
+            x, info = qp_ipm.osqp_like_solve(self.prob)
+            CURRENT["captured"] = (self.prob, x, info, self.kw)
+            return types.SimpleNamespace(x=x, info=types.SimpleNamespace(status_val=info["status_val"]))
+
+    oq.OSQP = OSQP
+    sys.modules["osqp"] = oq
+    sys.path.insert(0, REF)
+
+
+def ref_cone_boost(mpc):
+    """Same rule as ``oracle.tree.CVaRController.cone_boost`` on the reference's own tree."""
+    out = []
+    q = [mpc.BT]
+    while q:
+        br = q.pop(0)
+        if br.depth < mpc.NB:
+            for ch in br.children:
+                est = 0.0
+                for j in range(ch.xtraj.shape[0]):
+                    est += ch.xtraj[j] @ mpc.Q @ ch.xtraj[j] + ch.utraj[j] @ mpc.R @ ch.utraj[j]
+                out.append(0.5 * np.log(max(1.0, est)))
+                q.append(ch)
+    u0 = mpc.BT.utraj[0]
+    out.append(0.5 * np.log(max(1.0, u0 @ mpc.R @ u0)))
+    return out
+
+
+def coo(M, name, d):
+    M = sp.coo_matrix(M)
+    d[name + "_data"] = M.data
+    d[name + "_row"] = M.row.astype(np.int32)
+    d[name + "_col"] = M.col.astype(np.int32)
+    d[name + "_shape"] = np.array(M.shape, np.int64)
+
+
+def bt_arrays(mpc):
+    xs, zs, us, ws = mpc.BT2array()[:4]
+    return np.array(xs), np.array(zs), np.array(us), np.array(ws)
+
+
+def gen_highway(name, N, NB, steps, keep, out):
+    import Init_MPC
+    import MPC_branch
+    from utils import Branch_constants
+
+    n, d, dt, am, rm, N_lane = 4, 2, 0.1, 6.0, 0.3, 4
+    xRef0 = np.array([0.5, 1.8, 15, 0])
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
+                            s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
+    mpc = MPC_branch.BranchMPC_CVaR(param, model, ralpha=0.9)
+    CURRENT["mpc"] = mpc
+    env = HighwayOvertake(mpc, model, N_lane=N_lane, L=cons.L, W=cons.W, Kpsi=cons.Kpsi,
+                          lc_target0=xRef0, dt=dt)
+    d_out = dict(N=N, NB=NB, m=3, n=n, d=d, dt=dt, am=am, rm=rm, N_lane=N_lane, ralpha=0.9,
+                 L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef0,
+                 Q=param.Q, R=param.R, Fx=param.Fx, bx=np.asarray(param.bx, float).reshape(-1),
+                 Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "exit", "J", "iters", "collision")}
+    t0 = time.time()
+    for t in range(steps):
+        if not env.collision:
+            env.check_collision()
+        r = env.step(t)
+        prob, sol, info, kw = CURRENT["captured"]
+        assert kw == {"verbose": False}, kw
+        for k in ("x", "z", "xRef", "u", "lc_target"):
+            traj[k].append(r[k])
+        traj["exit"].append(info["exitFlag"])
+        traj["J"].append(sol[-1])
+        traj["iters"].append(info["iter"])
+        traj["collision"].append(env.collision)
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.G, p + "G", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "c"] = prob.c
+            d_out[p + "h"] = prob.h
+            d_out[p + "b"] = prob.b
+            d_out[p + "dims_l"] = np.array(prob.dims["l"])
+            d_out[p + "dims_q"] = np.array(prob.dims["q"])
+            d_out[p + "cone_boost"] = np.array(prob.cone_boost)
+            d_out[p + "sol"] = sol
+            d_out[p + "exit"] = np.array(info["exitFlag"])
+            d_out[p + "uPred"] = mpc.uPred
+            d_out[p + "xPred"] = mpc.xPred
+            d_out[p + "uLin_prev"] = np.zeros(1) if t == 0 else d_out.get("_uLin_prev", np.zeros(1))
+            xs, zs, us, ws = bt_arrays(mpc)
+            d_out[p + "bt_x"], d_out[p + "bt_z"], d_out[p + "bt_u"], d_out[p + "bt_w"] = xs, zs, us, ws
+        print(f"[{name}] t={t:3d} exit={info['exitFlag']:3d} it={info['iter']:3d} J={sol[-1]:.6f} "
+              f"u0={mpc.uPred[0]} ({time.time() - t0:.0f}s)", flush=True)
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
+def gen_quadruped(name, steps, keep, out):
+    import Init_MPC
+    import MPC_branch
+
+    n, d, N, NB, dt = 3, 3, 25, 2, 0.2
+    vxm, vym, rm, v0 = 0.2, 0.1, 0.5, 0.2
+    L1, L2, W1, W2, col_tol = 0.5, 1.0, 0.3, 0.6, 0.2
+    xRef = np.array([5., 5., 0.])
+    model = QuadrupedModel(N, dt, quadruped_policies(v0), L1=L1, W1=W1, L2=L2, W2=W2, col_tol=col_tol, s1=2.0)
+    param = Init_MPC.initquadBranchMPC(n, d, N, NB, xRef, vxm, vym, rm)
+    mpc = MPC_branch.BranchMPCProx(param, model)
+    CURRENT["mpc"] = mpc
+    d_out = dict(N=N, NB=NB, m=2, n=n, d=d, dt=dt, vxm=vxm, vym=vym, rm=rm, v0=v0, L1=L1, L2=L2, W1=W1,
+                 W2=W2, col_tol=col_tol, Q=param.Q, R=param.R, dR=param.dR,
+                 Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack, xRef0=xRef)
+    # the build's own quadruped loop (quadruped_env.py:67-130 crashes at :120; same rules)
+    x_des = np.array([5., -3., 0.])
+    ego = np.array([0, 1.8, 0.]); obs = np.array([2.5, 2.5, -np.pi / 2])
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "status")}
+    for t in range(steps):
+        dx = x_des[0:2] - ego[0:2]
+        dx = dx / np.linalg.norm(dx) * min(np.linalg.norm(dx), 5.0)
+        if np.linalg.norm(dx) > 0.1:
+            psiRef = np.arctan2(dx[1], dx[0])
+            while psiRef - x_des[2] > np.pi:
+                psiRef -= 2 * np.pi
+            while psiRef - x_des[2] < -np.pi:
+                psiRef += 2 * np.pi
+        else:
+            psiRef = ego[2]
+        xr = ego.copy(); xr[0:2] += dx; xr[2] = psiRef
+        mpc.solve(ego.copy(), obs.copy(), xr)
+        prob, sol, info, kw = CURRENT["captured"]
+        assert kw == {"verbose": False, "polish": True}, kw
+        u = mpc.uPred[0].copy()
+        traj["x"].append(ego.copy()); traj["z"].append(obs.copy()); traj["xRef"].append(xr)
+        traj["u"].append(u); traj["status"].append(info["status_val"])
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.P, p + "P", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "q"] = prob.q
+            d_out[p + "l"] = prob.l
+            d_out[p + "u"] = prob.u
+            d_out[p + "sol"] = sol
+            d_out[p + "uPred"] = mpc.uPred
+            d_out[p + "xPred"] = mpc.xPred
+            xs, zs, us, ws = bt_arrays(mpc)
+            d_out[p + "bt_x"], d_out[p + "bt_z"], d_out[p + "bt_u"], d_out[p + "bt_w"] = xs, zs, us, ws
+        # robot.step (quadruped_env.py:34-37); obstacle: forward policy (v0) as chosen by
+        # the env's rule when the L2 clearance of the forward branch exceeds 0.5
+        ego = ego + np.array([u[0] * np.cos(ego[2]) - u[1] * np.sin(ego[2]),
+                              u[1] * np.cos(ego[2]) + u[0] * np.sin(ego[2]), u[2]]) * dt
+        uo = np.array([v0, 0, 0])
+        obs = obs + np.array([uo[0] * np.cos(obs[2]) - uo[1] * np.sin(obs[2]),
+                              uo[1] * np.cos(obs[2]) + uo[0] * np.sin(obs[2]), uo[2]]) * dt
+        print(f"[{name}] t={t} status={info['status_val']} u0={u}", flush=True)
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="")
+    ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    a = ap.parse_args()
+    install_stubs()
+    out = a.out
+    os.makedirs(out, exist_ok=True)
+    jobs = {
+        "highway_n20_nb1": lambda: gen_highway("highway_n20_nb1", 20, 1, 8 if a.quick else 100, {0, 1, 2, 5, 50}, out),
+        "highway_n8_nb2": lambda: gen_highway("highway_n8_nb2", 8, 2, 5 if a.quick else 40, {0, 1, 2, 30}, out),
+        "highway_n10_nb1": lambda: gen_highway("highway_n10_nb1", 10, 1, 5 if a.quick else 20, {0, 1}, out),
+        "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 2, {0, 1}, out),
+        "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 10, {0, 1, 2}, out),
+    }
+    for k, f in jobs.items():
+        if a.only and k not in a.only.split(","):
+            continue
+        f()
+
+
+if __name__ == "__main__":
+    main()
