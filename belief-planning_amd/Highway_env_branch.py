@@ -1,0 +1,185 @@
+"""Highway closed-loop scene -- drop-in for the reference's ``Highway_env_branch`` module.
+
+Host-side driver of one ego (scalar ``mpc.solve`` per step) with the reference's rules
+(``Highway_env_branch.py:48-184,393-445,719-725``): obstacle policy selection with the
+NumPy ``veh_col`` / ``lane_bdry_h`` against the env boundary, obstacle inputs from the
+env's construction-time policy list, lane bookkeeping with round-half-even, lane-change
+re-targeting through ``update_backup``, the x_ref rule and Euler vehicle steps.
+Plotting/animation are out of scope (``animate_scenario`` and ``plot_snapshot`` only
+report that).  The batched, on-device version of this loop is ``bench.py``'s env step.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from highway_branch_dyn import backup_brake, backup_lc, backup_maintain, lane_bdry_h, veh_col
+
+v0 = 20
+f0 = np.array([v0, 0, 0, 0])
+lane_width = 3.6
+lm = np.arange(0, 7) * lane_width
+
+
+def with_probability(P=1):
+    return np.random.uniform() <= P
+
+
+class vehicle:
+    """Euler-integrated unicycle (:28-41)."""
+
+    def __init__(self, state=(0, 0, v0, 0), v_length=4, v_width=2.4, dt=0.05, backupidx=0, laneidx=0):
+        self.state = np.array(state, float)
+        self.dt, self.v_length, self.v_width = dt, v_length, v_width
+        self.x_pred, self.y_pred, self.xbackup = [], [], None
+        self.backupidx, self.laneidx = backupidx, laneidx
+
+    def step(self, u):
+        s = self.state
+        self.state = s + np.array([s[2] * np.cos(s[3]), s[2] * np.sin(s[3]), u[0], u[1]]) * self.dt
+
+
+class Highway_env:
+    """Overtake scene (:48-184)."""
+
+    def __init__(self, NV, mpc, N_lane=6):
+        self.dt = mpc.predictiveModel.dt
+        self.NV, self.N_lane, self.mpc = NV, N_lane, mpc
+        self.predictiveModel = mpc.predictiveModel
+        self.backupcons = mpc.predictiveModel.backupcons       # kept: later update_backup
+        self.m = len(self.backupcons)                            # replaces the model's list only
+        self.cons = mpc.predictiveModel.cons
+        self.LB = [self.cons.W / 2, N_lane * 3.6 - self.cons.W / 2]
+        x0 = np.array([[0, 1.8, v0, 0], [5, 5.4, v0, 0]], float)
+        self.veh_set = [vehicle(x0[i], dt=self.dt, backupidx=0) for i in range(NV)]
+        self.desired_x = [np.array([0, x0[i, 1], v0, 0], float) for i in range(NV)]
+
+    def _retarget(self):
+        """Lane-change target of the ego relative to the obstacle lane (:103-116)."""
+        l0, l1 = self.veh_set[0].laneidx, self.veh_set[1].laneidx
+        if l0 < l1 or (l0 == l1 and l1 > 0):
+            y = 1.8 + 3.6 * (l1 - 1)
+        else:
+            y = 1.8 + 3.6 * (l1 + 1)
+        return np.array([0, y, v0, 0], float)
+
+    def step(self, t_):
+        n = self.predictiveModel.n
+        xx_set = [None] * self.NV
+        for i, veh in enumerate(self.veh_set):
+            z = veh.state
+            xx_set[i] = self.predictiveModel.zpred_eval(z)
+            new = round((z[1] - 1.8) / 3.6)
+            if t_ == 0 or (new != veh.laneidx and abs(z[1] - 1.8 - 3.6 * new) < 1.4):
+                veh.laneidx = new
+                self.desired_x[i][1] = 1.8 + new * 3.6
+                if i == 1:
+                    tgt = self._retarget()
+                    cons = self.cons
+                    self.predictiveModel.update_backup([lambda x: backup_maintain(x, cons),
+                                                        lambda x: backup_brake(x, cons),
+                                                        lambda x: backup_lc(x, tgt)])
+            if t_ % 10 == 0 and i != 0 and with_probability(0.5):
+                pass   # the reference only rewrites desired_x here, which nothing reads (:121-133)
+        ego = self.veh_set[0]
+        x1 = xx_set[0][:, ego.backupidx * n:(ego.backupidx + 1) * n]
+        u0_set = [None] * self.NV
+        for i in range(1, self.NV):
+            hi = np.array([min(np.append(veh_col(x1, xx_set[i][:, j * n:(j + 1) * n],
+                                                 [self.cons.L + 1, self.cons.W + 0.2]),
+                                         lane_bdry_h(x1, self.LB[0], self.LB[1]))) for j in range(self.m)])
+            self.veh_set[i].backupidx = int(np.argmax(hi))
+            u0_set[i] = self.backupcons[self.veh_set[i].backupidx](self.veh_set[i].state)
+        e, o = self.veh_set[0].state, self.veh_set[1].state
+        Ydes = 1.8 + ego.laneidx * 3.6 if e[0] < o[0] else o[1]
+        vdes = v0 if (abs(e[1] - Ydes) < 1 and e[0] > o[0] + 3) else o[2] + 1 * (o[0] + 1.5 - e[0])
+        xRef = np.array([0, Ydes, vdes, 0], float)
+        self.mpc.solve(e, o, xRef)
+        u_set = [self.mpc.uPred[0]] + u0_set[1:]
+        xPred, zPred, uPred, branch_w = self.mpc.BT2array()
+        ego.step(u_set[0])
+        for i in range(1, self.NV):
+            self.veh_set[i].step(u_set[i])
+        x_set = [v.state for v in self.veh_set]
+        return u_set, x_set, xx_set, xPred, zPred, branch_w
+
+
+def Highway_sim(env, T):
+    """Closed loop of T seconds (:393-445); returns the reference's record tuple."""
+    collision = False
+    N = int(round(T / env.dt))
+    state_rec = np.zeros([env.NV, N, 4])
+    input_rec = np.zeros([env.NV, N, 2])
+    backup_rec = [[None] * N for _ in range(env.NV)]
+    backup_choice_rec = [[None] * N for _ in range(env.NV)]
+    xPred_rec, zPred_rec, branch_w_rec = [None] * N, [None] * N, [None] * N
+    for i, veh in enumerate(env.veh_set):
+        state_rec[i][0] = veh.state
+    dis = 100
+    for t in range(N):
+        if not collision:
+            for i in range(env.NV):
+                for j in range(env.NV):
+                    if i != j:
+                        a, b = env.veh_set[i], env.veh_set[j]
+                        dis = max(abs(a.state[0] - b.state[0]) - 0.5 * (a.v_length + b.v_length),
+                                  abs(a.state[1] - b.state[1]) - 0.5 * (a.v_width + b.v_width))
+            if dis < 0:       # the reference tests only the last pair's distance (:427)
+                collision = True
+        u_set, x_set, xx_set, xPred, zPred, branch_w = env.step(t)
+        xPred_rec[t], zPred_rec[t], branch_w_rec[t] = xPred, zPred, branch_w
+        for i in range(env.NV):
+            input_rec[i][t] = u_set[i]
+            state_rec[i][t] = x_set[i]
+            backup_rec[i][t] = xx_set[i]
+            backup_choice_rec[i][t] = env.veh_set[i].backupidx
+    return state_rec, input_rec, backup_rec, backup_choice_rec, xPred_rec, zPred_rec, branch_w_rec, collision
+
+
+def merge_geometry(N_lane, merge_lane, merge_s, merge_R, merge_side=0):
+    """Ramp geometry of the merge scene (:447-...): straight lead-in + circular arc."""
+    th = np.arccos(1 - lane_width * merge_lane / merge_R)
+    if merge_side == 0:
+        center = np.array([merge_s + merge_R * np.sin(th), (N_lane - merge_lane) * lane_width + merge_R])
+        start = np.array([merge_s - merge_s * np.cos(th), N_lane * lane_width + np.sin(th) * merge_s])
+    else:
+        center = np.array([merge_s + merge_R * np.sin(th), merge_lane * lane_width - merge_R])
+        start = np.array([merge_s - merge_s * np.cos(th), -np.sin(th) * merge_s - lane_width * merge_lane])
+    s1 = np.linspace(0, merge_s, num=int(merge_s / 0.5), endpoint=False)
+    s2 = merge_s + np.linspace(0, merge_R * th, num=int(merge_R * th / 0.5))
+    sgn = 1.0 if merge_side == 0 else -1.0
+    X1 = start[0] + s1 * np.cos(th)
+    Y1 = start[1] - sgn * s1 * np.sin(th)
+    psi1 = -sgn * np.ones(s1.shape) * th
+    psi2 = sgn * (s2 - s2[-1]) / merge_R
+    X2 = center[0] + sgn * np.sin(psi2) * merge_R
+    if merge_side == 0:
+        Y2 = center[1] - np.cos(psi2) * merge_R
+    else:
+        Y2 = center[1] + np.cos(psi2) * merge_R - merge_lane * lane_width
+    return X1, X2, Y1, Y2, psi1, psi2
+
+
+def plot_snapshot(*args, **kwargs):
+    """Plotting is out of scope for the MI355X build (matplotlib snapshot, :447)."""
+    return None
+
+
+def animate_scenario(*args, **kwargs):
+    """Animation is out of scope for the MI355X build (:566-709)."""
+    print("[Highway_env_branch] animate_scenario: plotting is not part of the MI355X build; skipped")
+    return None
+
+
+def sim_overtake(mpc, N_lane):
+    """The main_branch.py scene (:719-725): 2 vehicles, 10 s; returns the records."""
+    env = Highway_env(NV=2, mpc=mpc, N_lane=N_lane)
+    rec = Highway_sim(env, 10)
+    state_rec, input_rec, backup_rec, backup_choice_rec, xPred_rec, zPred_rec, branch_w_rec, collision = rec
+    animate_scenario(env, state_rec, backup_rec, backup_choice_rec, xPred_rec, zPred_rec, lm)
+    return rec
+
+
+def sim_merge(*args, **kwargs):
+    raise NotImplementedError("the merge scene (PredictiveModel_merge) is not built yet")

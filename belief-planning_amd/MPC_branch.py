@@ -1,0 +1,261 @@
+"""Branch-MPC controllers -- drop-in for the reference's ``MPC_branch`` module.
+
+``BranchMPC_CVaR`` keeps the reference's constructor, ``solve`` signature and the
+attributes drivers read (``uPred``, ``xPred``, ``xLin``, ``uLin``, ``feasible``,
+``solverTime``, ``OldInput``, ``BT``, ``BT2array()``, ``psimax``, ...), but one solve is
+one call into libbmpc.so: the tree update, linearisation, SOCP assembly and the
+interior-point solve all run in the gfx950 kernels (one wavefront per ego).  Passing
+``batch=B`` to the constructor turns the object into a B-ego controller
+(``solve_batch``).  There is no CPU fallback: without a HIP device the first solve raises
+``bmpc._lib.BmpcUnavailable``.
+"""
+from __future__ import annotations
+
+import datetime
+from dataclasses import dataclass, field, fields
+
+import numpy as np
+from scipy import linalg
+
+from bmpc import abi
+from bmpc.topology import TreeIndex
+
+
+@dataclass
+class PythonMsg:
+    def __setattr__(self, key, value):
+        if key not in {f.name for f in fields(self)} and not hasattr(self, key):
+            raise TypeError(f'Cannot add new field "{key}" to frozen class {self}')
+        object.__setattr__(self, key, value)
+
+
+@dataclass
+class BranchMPCParams(PythonMsg):
+    """Branch-MPC parameters (MPC_branch.py:27-54); Qf defaults to Q."""
+
+    n: int = field(default=None)
+    d: int = field(default=None)
+    NB: int = field(default=None)
+    N: int = field(default=None)
+    A: np.ndarray = field(default=None)
+    B: np.ndarray = field(default=None)
+    Q: np.ndarray = field(default=None)
+    R: np.ndarray = field(default=None)
+    Qf: np.ndarray = field(default=None)
+    dR: np.ndarray = field(default=None)
+    Qslack: np.ndarray = field(default=None)
+    Fx: np.ndarray = field(default=None)
+    bx: np.ndarray = field(default=None)
+    Fu: np.ndarray = field(default=None)
+    bu: np.ndarray = field(default=None)
+    xRef: np.ndarray = field(default=None)
+    slacks: bool = field(default=True)
+    timeVarying: bool = field(default=False)
+
+    def __post_init__(self):
+        if self.Qf is None:
+            self.Qf = self.Q
+        if self.dR is None:
+            self.dR = np.zeros(self.d)
+        if self.xRef is None:
+            self.xRef = np.zeros(self.n)
+
+
+class BranchTree:
+    """One branch of the scenario tree (MPC_branch.py:65-78), filled from the GPU tree."""
+
+    def __init__(self, xtraj, ztraj, utraj, w, depth=0):
+        self.xtraj, self.ztraj, self.utraj = xtraj, ztraj, utraj
+        self.dynmatr = [None] * xtraj.shape[0]
+        self.w = w
+        self.children = []
+        self.depth = depth
+        self.p = None
+        self.dp = None
+        self.J = 0
+
+    def addchild(self, BT):
+        self.children.append(BT)
+
+
+def _weight_root(M):
+    """cholesky(M).T with the sqrtm fallback (MPC_branch.py:1628-1643)."""
+    try:
+        return np.linalg.cholesky(M).T
+    except np.linalg.LinAlgError:
+        return np.real(linalg.sqrtm(M))
+
+
+def _flat_bx(bx):
+    return np.asarray(bx[0] if isinstance(bx, tuple) else bx, float).reshape(-1)
+
+
+class BranchMPC_CVaR:
+    """Branch MPC with a CVaR objective (MPC_branch.py:1598-2152) on MI355X."""
+
+    controller_kind = abi.CTRL_CVAR
+
+    def __init__(self, mpcParameters, predictiveModel, ralpha, S=None, batch=1, device=0):
+        p = mpcParameters
+        self.N, self.NB, self.n, self.d = p.N, p.NB, p.n, p.d
+        self.Qslack, self.Q, self.Qf, self.R, self.dR = p.Qslack, p.Q, p.Qf, p.R, p.dR
+        self.Fx, self.Fu, self.bx, self.bu = p.Fx, p.Fu, p.bx, p.bu
+        self.xRef = p.xRef
+        self.m = predictiveModel.m
+        self.psimax = p.bx[0][2][0] if np.size(_flat_bx(p.bx)) > 2 else None
+        self.S = S
+        self.ralpha = ralpha
+        self.param = p
+        self.Wx = _weight_root(np.asarray(self.Q, float))
+        self.Wu = _weight_root(np.asarray(self.R, float))
+        if self.dR is not None:
+            self.Wdu = _weight_root(np.diag(np.asarray(self.dR, float)))
+        self.slacks, self.timeVarying = p.slacks, p.timeVarying
+        self.predictiveModel = predictiveModel
+        self.batch, self.device = int(batch), device
+        self.tree_index = TreeIndex(self.N, self.NB, self.m)
+        self.totalx, self.totalu = self.tree_index.T, self.tree_index.U
+        self.branchdim = self.tree_index.bdim
+        self.BT = None
+        self.xPred = self.uPred = self.xLin = self.uLin = None
+        self.OldInput = np.zeros(self.d)
+        self.feasible = 0
+        self.J = None
+        self.status = None
+        self.iters = None
+        zero = datetime.timedelta(0)
+        self.solverTime = zero
+        self.linearizationTime = zero
+        self.timeStep = 0
+        self._plan = None
+        self._pol_rows = None
+        self._last = None
+
+    # ---- plan ------------------------------------------------------------------------------
+    def plan_desc(self):
+        mdl = self.predictiveModel
+        Fx = np.asarray(self.Fx, float).reshape(-1, self.n)
+        return abi.make_desc(self.controller_kind, mdl.model_kind, self.n, self.d, self.N, self.NB, self.m,
+                             mdl.dt, self.Q, self.R, Fx, _flat_bx(self.bx), self.Fu,
+                             np.asarray(self.bu, float).reshape(-1), self.Qslack, mdl.model_constants(),
+                             ralpha=self.ralpha, Qf=self.Qf, dR=self.dR)
+
+    def _ensure_plan(self):
+        if self._plan is None:
+            from bmpc.plan import BatchPlan
+            self._plan = BatchPlan(self.plan_desc(), self.batch, self.device)
+        rows = self.predictiveModel.policy_rows()
+        if rows != self._pol_rows:               # update_backup happened
+            self._plan.set_policies([rows] * self.batch)
+            self._pol_rows = rows
+        return self._plan
+
+    # ---- solve -----------------------------------------------------------------------------
+    def solve(self, x, z, xRef=None, S=None, Fx=None, bx=None):
+        """One controller step (MPC_branch.py:2043-2092)."""
+        if S is not None or Fx is not None or bx is not None:
+            raise NotImplementedError("state transformation S / per-step Fx, bx (merge scene) not built yet")
+        if self.batch != 1:
+            raise ValueError("this controller holds a batch; use solve_batch")
+        if xRef is not None:
+            self.xRef = xRef
+        pl = self._ensure_plan()
+        t0 = datetime.datetime.now()
+        r = pl.solve(np.asarray(x, float)[None], np.asarray(z, float)[None],
+                     np.asarray(self.xRef, float)[None])
+        self.solverTime = datetime.datetime.now() - t0
+        self._unpack(r, 0)
+        self.timeStep += 1
+
+    def _unpack(self, r, e):
+        self._last = r
+        st = int(r["status"][e])
+        self.status, self.iters, self.J = st, int(r["iters"][e]), float(r["J"][e])
+        self.feasible = 1 if st >= 0 else 0       # ECOS exitFlag >= 0 (MPC_branch.py:2141)
+        # the library keeps the previous prediction when a solve is infeasible (:2098)
+        self.xPred = r["xpred"][e]
+        self.uPred = r["upred"][e]
+        self.xLin = self.xPred
+        self.uLin = np.vstack((self.uPred, self.uPred[-1]))
+        self.OldInput = self.uPred[0, :]
+        self.BT = None
+        self._tree = None
+
+    def solve_batch(self, X, Z, XREF):
+        """Batched step for all egos of the plan: returns the raw result dict
+        (upred [B,U,d], xpred [B,T,n], branch_w, J, status, iters)."""
+        pl = self._ensure_plan()
+        t0 = datetime.datetime.now()
+        r = pl.solve(X, Z, XREF)
+        self.solverTime = datetime.datetime.now() - t0
+        self._last = r
+        self.timeStep += 1
+        return r
+
+    # ---- scenario tree views ------------------------------------------------------------------
+    def _tree_arrays(self, e=0):
+        if getattr(self, "_tree", None) is None:
+            self._tree = self._plan.tree()
+        return {k: v[e] for k, v in self._tree.items()}
+
+    def BT2array(self, e=0):
+        """(xtraj, ztraj, utraj, branch_w) over non-root branches, BFS order (:2108-2122)."""
+        t = self.tree_index
+        a = self._tree_arrays(e)
+        xs, zs, us, ws = [], [], [], []
+        for b in range(t.nbranch):
+            lx, lu = t.ndx[b] + t.length[b] - 1, t.ndu[b] + t.length[b] - 1
+            for c in t.children[b]:
+                sl = slice(t.ndx[c], t.ndx[c] + t.N)
+                su = slice(t.ndu[c], t.ndu[c] + t.N)
+                ws.append(a["w"][c])
+                xs.append(np.vstack((a["xbar"][lx], a["xbar"][sl])))
+                zs.append(np.vstack((a["zbar"][lx], a["zbar"][sl])))
+                us.append(np.vstack((a["ubar"][lu], a["ubar"][su])))
+        return xs, zs, us, ws
+
+    def build_tree(self, e=0):
+        """BranchTree objects of the last solve (the reference's ``self.BT``)."""
+        t = self.tree_index
+        a = self._tree_arrays(e)
+        nodes = []
+        for b in range(t.nbranch):
+            sl = slice(t.ndx[b], t.ndx[b] + t.length[b])
+            su = slice(t.ndu[b], t.ndu[b] + t.length[b])
+            br = BranchTree(a["xbar"][sl].copy(), a["zbar"][sl].copy(), a["ubar"][su].copy(), a["w"][b],
+                            t.depth[b])
+            if not t.is_leaf(b):
+                br.p = a["p"][b].copy()
+            nodes.append(br)
+        for b in range(t.nbranch):
+            for c in t.children[b]:
+                nodes[b].addchild(nodes[c])
+        self.BT = nodes[0]
+        return self.BT
+
+    @property
+    def Solution(self):
+        return self._tree_arrays()["sol"]
+
+
+class _NotBuilt:
+    _what = ""
+
+    def __init__(self, *args, **kwargs):
+        raise NotImplementedError(f"{self._what} is not built in this version of the MI355X library "
+                                  "(see DESIGN.md, scope)")
+
+
+class BranchMPCProx(_NotBuilt):
+    """Proximal branch QP (MPC_branch.py:82-488) -- next row of SURVEY §8."""
+    _what = "BranchMPCProx (quadruped QP)"
+
+
+class BranchMPC(_NotBuilt):
+    """Branch QP (MPC_branch.py:881-1274)."""
+    _what = "BranchMPC"
+
+
+class robustMPC(_NotBuilt):
+    """Robust branch QP (MPC_branch.py:1275-1595)."""
+    _what = "robustMPC"

@@ -62,6 +62,8 @@ _SIGS = {
     "bmpc_solve": (C.c_int, [C.c_void_p] + [C.c_void_p] * 9),
     "bmpc_solve_device": (C.c_int, [C.c_void_p] + [C.c_void_p] * 10),
     "bmpc_get_tree": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
+    "bmpc_get_warm_start": (C.c_int, [C.c_void_p] * 4),
+    "bmpc_set_warm_start": (C.c_int, [C.c_void_p] * 5),
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),

@@ -84,6 +84,24 @@ class BatchPlan:
                                                      bw_ptr, J_ptr, status_ptr, iters_ptr, stream)]
         check(lib().bmpc_solve_device(self._h, *vp), "bmpc_solve_device")
 
+    def get_warm_start(self):
+        """Checkpoint of the per-ego warm start (uLin, p, Jcons)."""
+        B, d = self.batch, self.desc.d
+        uLin = np.zeros((B, self.U + 1, d))
+        p = np.zeros((B, self.bdim, self.desc.m))
+        jc = np.zeros(B)
+        check(lib().bmpc_get_warm_start(self._h, _p(uLin), _p(p), _p(jc)), "bmpc_get_warm_start")
+        return dict(uLin=uLin, p=p, jcons=jc)
+
+    def set_warm_start(self, uLin, p, jcons, mask=None):
+        """Resume from a checkpoint (the next solve runs updatetree)."""
+        B, d = self.batch, self.desc.d
+        uLin = np.ascontiguousarray(np.asarray(uLin, np.float64).reshape(B, self.U + 1, d))
+        p = np.ascontiguousarray(np.asarray(p, np.float64).reshape(B, self.bdim, self.desc.m))
+        jc = np.ascontiguousarray(np.asarray(jcons, np.float64).reshape(B))
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_set_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(m)), "bmpc_set_warm_start")
+
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d
         out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),

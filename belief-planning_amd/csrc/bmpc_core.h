@@ -13,6 +13,7 @@
 #include "bmpc.h"
 
 #if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define BMPC_HD __host__ __device__ __forceinline__
 #else
 #define BMPC_HD inline

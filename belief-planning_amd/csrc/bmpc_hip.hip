@@ -95,6 +95,15 @@ __global__ void k_gather(const double* __restrict__ ws, size_t stride, size_t of
   }
 }
 
+__global__ void k_scatter(double* __restrict__ ws, size_t stride, size_t off, int count,
+                          const double* __restrict__ in, const uint8_t* __restrict__ mask, int batch) {
+  const size_t tot = (size_t)batch * count;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i / count, j = i % count;
+    if (!mask || mask[e]) ws[e * stride + off + j] = in[i];
+  }
+}
+
 __global__ void k_reset(double* ws, size_t stride, size_t off, const uint8_t* mask, int batch) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e < batch && (!mask || mask[e])) ws[e * stride + off + MISC_INIT] = 0.0;
@@ -377,6 +386,52 @@ static int gather(bmpc_plan* pl, size_t off, int count, double* host) {
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemcpyAsync(host, pl->d_scratch, need * sizeof(double), hipMemcpyDeviceToHost, pl->stream));
   HIPCHECK(hipStreamSynchronize(pl->stream));
+  return 0;
+}
+
+int bmpc_get_warm_start(bmpc_plan* pl, double* uLin, double* p, double* jcons) {
+  if (!pl) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  int rc;
+  if ((rc = gather(pl, L.uLin, (P.U + 1) * P.d, uLin))) return rc;
+  if (P.bdim * P.m > 0 && (rc = gather(pl, L.pprev, P.bdim * P.m, p))) return rc;
+  if ((rc = gather(pl, L.misc + MISC_JCONS, 1, jcons))) return rc;
+  return 0;
+}
+
+int bmpc_set_warm_start(bmpc_plan* pl, const double* uLin, const double* p, const double* jcons,
+                        const uint8_t* mask) {
+  if (!pl || !uLin || !jcons) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  const int B = pl->batch;
+  const int cu = (P.U + 1) * P.d, cp = P.bdim * P.m;
+  const size_t need = (size_t)B * (cu + cp + 2);
+  double* buf = nullptr;
+  uint8_t* dmask = nullptr;
+  HIPCHECK(hipMalloc(&buf, need * sizeof(double)));
+  if (mask) HIPCHECK(hipMalloc(&dmask, B));
+  std::vector<double> ones(B, 1.0);
+  HIPCHECK(hipMemcpy(buf, uLin, sizeof(double) * B * cu, hipMemcpyHostToDevice));
+  if (cp && p) HIPCHECK(hipMemcpy(buf + (size_t)B * cu, p, sizeof(double) * B * cp, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(buf + (size_t)B * (cu + cp), jcons, sizeof(double) * B, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(buf + (size_t)B * (cu + cp + 1), ones.data(), sizeof(double) * B, hipMemcpyHostToDevice));
+  if (mask) HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.uLin, cu, buf, dmask, B);
+  if (cp && p)
+    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.pprev, cp,
+                       buf + (size_t)B * cu, dmask, B);
+  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.misc + MISC_JCONS, 1,
+                     buf + (size_t)B * (cu + cp), dmask, B);
+  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.misc + MISC_INIT, 1,
+                     buf + (size_t)B * (cu + cp + 1), dmask, B);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  hipFree(buf);
+  if (dmask) hipFree(dmask);
   return 0;
 }
 

@@ -1197,6 +1197,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
   const double resy0 = fmax(1.0, sqrt(vdot(ex, bv, bv, neq)));
   const double resz0 = fmax(1.0, sqrt(vdot(ex, hv, hv, nr)));
   double best_score = 1e300, best_tau = 1.0;
+  int stall = 0;
   int best_it = 0;
   double bs_pres = 0, bs_dres = 0, bs_relgap = 0, bs_gap = 0, bs_pcost = 0;
   bool bs_ok_cx = false;
@@ -1244,6 +1245,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       dinfres = fmax(a1, a2);
     }
     auto check = [&](double ft, double at, double rtl) -> int {
+      if (!(tau > 0.0 && kap >= 0.0)) return 99;
       if ((-cx > 0.0 || -by - hz >= -at) && pres < ft && dres < ft &&
           (gap < at || (relgap >= 0.0 && relgap < rtl)))
         return EXIT_OPTIMAL;
@@ -1254,6 +1256,9 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       return 99;
     };
     const double score = fmax(fmax(pres, dres), relgap >= 0.0 ? relgap : 1e300);
+    // stall counter: only in the end game (best iterate within the inaccurate tolerances)
+    if (score < 0.5 * best_score || best_score > 1e-4) stall = 0;
+    else ++stall;
     if (score < best_score) {
       best_score = score;
       best_it = it;
@@ -1263,7 +1268,25 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.bestx + i] = x[i];
       ex.sync();
     }
+#ifdef BMPC_HOST_DEBUG
+    printf("it %3d pcost %+.9e dcost %+.9e gap %.2e pres %.2e dres %.2e k/t %.2e tau %.2e nx %.2e\n", it, pcost,
+           dcost, gap, pres, dres, kap / tau, tau, nx);
+#endif
     int code = check(feastol, abstol, reltol);
+    if (code == 99 && stall >= 5) {    // no progress for 5 end-game iterations: precision floor
+      const int c2 = check(1e-4, 5e-5, 5e-5);
+      if (c2 != 99) code = c2 + EXIT_INACC;
+      else if (best_score < 1e300) {
+        const bool inacc = bs_ok_cx && bs_pres < 1e-4 && bs_dres < 1e-4 &&
+                           (bs_gap < 5e-5 || (bs_relgap >= 0.0 && bs_relgap < 5e-5));
+        for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.sol + i] = ws[L.bestx + i] / best_tau;
+        ex.sync();
+        res.exit_flag = inacc ? EXIT_OPTIMAL + EXIT_INACC : EXIT_MAXIT;
+        res.iters = it;
+        res.pcost = bs_pcost;
+        return res;
+      }
+    }
     if (code == 99 && it == P.desc.maxit) {
       const int c2 = check(1e-4, 5e-5, 5e-5);
       code = c2 == 99 ? EXIT_MAXIT : c2 + EXIT_INACC;
@@ -1305,8 +1328,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       double a_aff = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
       if (dtau_a < 0.0) a_aff = fmin(a_aff, -tau / dtau_a);
       if (dkap_a < 0.0) a_aff = fmin(a_aff, -kap / dkap_a);
-      a_aff = fmin(a_aff, 0.999);
-      a_aff = a_aff < 1e300 ? fmax(a_aff, 1e-6) : 0.999;
+      a_aff = fmax(0.0, fmin(a_aff, 0.999));
       double sigma = (1.0 - a_aff) * (1.0 - a_aff) * (1.0 - a_aff);
       sigma = fmin(1.0, fmax(1e-4, sigma));
       const double eta1 = 1.0 - sigma;
@@ -1339,13 +1361,12 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       if (dtau < 0.0) a = fmin(a, -tau / dtau);
       if (dkap < 0.0) a = fmin(a, -kap / dkap);
       a = fmin(a, 0.999);
-      a = a < 1e300 ? fmax(a, 1e-6) : 0.999;
-      alpha = a * 0.99;
+      alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
       apply_W(ex, C, 0, ds, rb);                               // ds = W dsW
       double fin = 0.0;
       for (int i = ex.lane; i < nv; i += ex.nlanes) fin += isfinite(x2[i]) ? 0.0 : 1.0;
       fin = ex.max(fin);
-      ok = fin == 0.0 && isfinite(dtau);
+      ok = fin == 0.0 && isfinite(dtau) && alpha > 1e-10;
       if (ok) {
         for (int i = ex.lane; i < nv; i += ex.nlanes) x[i] += alpha * x2[i];
         for (int i = ex.lane; i < neq; i += ex.nlanes) y[i] += alpha * y2[i];

@@ -1,0 +1,236 @@
+"""Headline benchmark: branch-MPC solves/sec, highway N=20, 3 branches, 4096 egos per GPU.
+
+One step = one closed-loop step of every ego: the batched BranchMPC_CVaR solve (tree update,
+linearisation, structured IPM) followed by the device-side Euler step of ego and obstacle
+and the x_ref rule of Highway_env.step.  Inputs stay in HBM (torch tensors on cuda).
+Multi-GPU: one process per GPU, egos sharded (weak scaling), one RCCL all-reduce of the
+closed-loop statistics per episode.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "belief-planning_amd"), os.path.join(REPO, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "branch-MPC solves/sec (whole node), highway N=20 M=3 branches, batch 4096 egos"
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector (= FP64 matrix) peak, spec
+
+
+def flops_per_iter(T, n, d, Nc, nFu, cone_dims):
+    """SURVEY §8(d) F_iter (transcendentals = 1)."""
+    per_node = (2 * (2 * n ** 3 + 3 * n ** 2 * d + 2 * n * d ** 2 + d ** 3 / 3.0) + 2 * Nc * n ** 2
+                + 4 * 2 * (2 * n ** 2 + 2 * n * d + d ** 2) + 2 * (2 * n ** 2 + 2 * n * d)
+                + 10 * (n + d + 2 * Nc + nFu))
+    return T * per_node + sum(20 * q for q in cone_dims)
+
+
+def flops_model(U, Bn, bdim, m, N, n):
+    """SURVEY §8(d) F_model."""
+    return (U + Bn) * 40 + bdim * (m * N * 60 + (2 * N * m * 50) * (1 + n)) + U * 30
+
+
+def cpu_baseline(N, NB, sample, procs):
+    """Oracle (NumPy restatement of the reference + ECOS-algorithm IPM) on host cores."""
+    import multiprocessing as mp
+    t0 = time.time()
+    with mp.get_context("spawn").Pool(procs, initializer=_worker_init) as pool:
+        res = pool.map(_cpu_solve, [(i, N, NB) for i in range(sample)])
+    dt = time.time() - t0
+    return dict(value=sample / dt, unit="solves/s", cores=procs, kind="port",
+                sample=f"{sample} first solves of seeded egos (seed 0) at N={N} NB={NB} m=3, "
+                       f"oracle/ (NumPy model+tree assembly, ECOS-algorithm IPM with sparse LU), "
+                       f"{procs} processes x 1 thread, {dt:.1f} s wall incl. pool start",
+                per_solve_s=float(np.mean([r for r in res])))
+
+
+def _worker_init():
+    os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    for _p in (REPO, os.path.join(REPO, "tests")):
+        if _p not in sys.path:
+            sys.path.insert(0, _p)
+
+
+def _cpu_solve(args):
+    i, N, NB = args
+    from common import seeded_batch
+    from oracle.ecos_ipm import ecos_solve
+    from oracle.model import HighwayModel, highway_policies
+    from oracle.tree import CVaRController
+    x, z, xref, tgt = seeded_batch(max(i + 1, 2), seed=0)
+    mdl = HighwayModel(N, 0.1, highway_policies(0.1, tgt[i]))
+    Fx = np.array([[0., 1, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1], [0, 0, 0, -1]])
+    c = CVaRController(mdl, N, NB, np.diag([0., 3, 3, 10]), np.diag([1., 100]), Fx,
+                       [4 * 3.6 - 1.25, -1.25, .25, .25], np.kron(np.eye(2), [1, -1]).T,
+                       [6., 6., .3, .3], [0, 300], xref[i], 0.9, solver=ecos_solve)
+    t0 = time.time()
+    c.solve(x[i], z[i], xref[i])
+    return time.time() - t0
+
+
+def load_traffic(path):
+    """Per-launch HBM bytes of the IPM kernel from a committed rocprofv3 --pmc summary."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("k_ipm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="egos per GPU")
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--NB", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=24)
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from bmpc import plan
+    from common import highway_desc, highway_policy_rows, seeded_batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B = a.batch
+    # shard: rank r owns egos [r*B, (r+1)*B) of one global seeded population
+    x, z, xref, tgt = seeded_batch(B, seed=1000 + rank) if rank else seeded_batch(B, seed=0)
+    desc = highway_desc(N=a.N, NB=a.NB)
+    pl = plan.BatchPlan(desc, B, device=local)
+    pl.set_policies(highway_policy_rows(tgt))
+    tx = torch.tensor(x, device=dev, dtype=torch.float64)
+    tz = torch.tensor(z, device=dev, dtype=torch.float64)
+    tr = torch.tensor(xref, device=dev, dtype=torch.float64)
+    up = torch.zeros((B, pl.U, 2), device=dev, dtype=torch.float64)
+    Jv = torch.zeros(B, device=dev, dtype=torch.float64)
+    st = torch.zeros(B, device=dev, dtype=torch.int32)
+    it = torch.zeros(B, device=dev, dtype=torch.int32)
+    stats = torch.zeros(8, device=dev, dtype=torch.float64)
+    stream = torch.cuda.current_stream(dev)
+    dt, v0 = 0.1, 20.0
+
+    def env_step():
+        """Euler step of ego (uPred[0]) and obstacle (maintain policy) + x_ref rule
+        (Highway_env_branch.py:39-41,153-167), on device."""
+        u0 = up[:, 0, :]
+        xs = tx
+        tx.copy_(xs + dt * torch.stack([xs[:, 2] * torch.cos(xs[:, 3]), xs[:, 2] * torch.sin(xs[:, 3]),
+                                         u0[:, 0], u0[:, 1]], 1))
+        zs = tz
+        tz.copy_(zs + dt * torch.stack([zs[:, 2] * torch.cos(zs[:, 3]), zs[:, 2] * torch.sin(zs[:, 3]),
+                                         torch.zeros_like(zs[:, 0]), -0.1 * zs[:, 3]], 1))
+        lane0 = torch.round((tx[:, 1] - 1.8) / 3.6)
+        Ydes = torch.where(tx[:, 0] < tz[:, 0], 1.8 + lane0 * 3.6, tz[:, 1])
+        vdes = torch.where((torch.abs(tx[:, 1] - Ydes) < 1) & (tx[:, 0] > tz[:, 0] + 3),
+                           torch.full_like(Ydes, v0), tz[:, 2] + (tz[:, 0] + 1.5 - tx[:, 0]))
+        tr[:, 1] = Ydes
+        tr[:, 2] = vdes
+        # closed-loop statistics (Highway_sim collision rule :421-429)
+        dis = torch.maximum(torch.abs(tx[:, 0] - tz[:, 0]) - 4.0, torch.abs(tx[:, 1] - tz[:, 1]) - 2.4)
+        stats[0] += Jv.sum()
+        stats[1] += (Jv * Jv).sum()
+        stats[2] += (st < 0).sum()
+        stats[3] += it.sum()
+        stats[4] += B
+        stats[5] += (dis < 0).sum()
+
+    def step():
+        pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
+                        Jv.data_ptr(), st.data_ptr(), it.data_ptr(), stream.cuda_stream)
+        env_step()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    stats.zero_()
+    # per-kernel device timing over separate instrumented steps (HIP events on the launch
+    # stream); the timed region below runs without event synchronisation
+    pl.enable_timing(True)
+    for _ in range(3):
+        step()
+    tm = pl.timing()
+    pl.enable_timing(False)
+    iters_mean = float(it.double().mean().item())
+    stats.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)   # the only collective
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total = B * world * a.steps
+    value = total / elapsed
+    if rank == 0:
+        st_h = stats.cpu().numpy()
+        T, U, bdim, nbr = pl.T, pl.U, pl.bdim, pl.nbranch
+        cone_dims = [2 + a.N * 6] * (bdim * 3) + [4]
+        F_it = flops_per_iter(T, 4, 2, 5, 4, cone_dims)
+        F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
+        achieved = B * iters_mean * F_it / (tm["ipm_ms"] * 1e-3) / 1e12 if tm["ipm_ms"] > 0 else 0.0
+        traffic = load_traffic(a.traffic)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)",
+            "config": {"workload": f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 "
+                                   f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
+                       "global_batch": B * world, "parallelism": f"ego-sharded dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
+                         "traffic": traffic,
+                         "kernel": "k_ipm (structured HSDE IPM)", "kernel_ms": round(tm["ipm_ms"], 4),
+                         "tree_kernel_ms": round(tm["tree_ms"], 4),
+                         "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
+                         "flop_model_per_solve": F_mod},
+            "closed_loop": {"J_mean": float(st_h[0] / max(st_h[4], 1)), "infeasible": int(st_h[2]),
+                            "iters_mean": float(st_h[3] / max(st_h[4], 1)), "collisions": int(st_h[5])},
+        }
+        if not a.no_cpu_baseline and world == 1:
+            procs = max(1, min(8, len(os.sched_getaffinity(0))))
+            cb = cpu_baseline(a.N, a.NB, a.cpu_sample, procs)
+            out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -153,6 +153,15 @@ int bmpc_solve_device(bmpc_plan* plan, const double* d_x, const double* d_z,
                       double* d_branch_w, double* d_J, int32_t* d_status,
                       int32_t* d_iters, void* stream);
 
+/* Checkpoint / resume of the per-ego warm start: the state the reference keeps
+ * in the controller object between solves -- uLin [batch][U+1][d] (shifted by updatetree,
+ * MPC_branch.py:1813-1823), the previous branch probabilities p [batch][bdim][m] (argmax
+ * child, :1818) and the frozen Jcons [batch] (:1939).  set marks the egos as initialised
+ * (the next solve runs updatetree, not inittree); mask NULL = all egos. */
+int bmpc_get_warm_start(bmpc_plan* plan, double* uLin, double* p, double* jcons);
+int bmpc_set_warm_start(bmpc_plan* plan, const double* uLin, const double* p,
+                        const double* jcons, const uint8_t* mask);
+
 /* Tree of the last solve (host copies; NULL skips):
  *   xbar,zbar [batch][T][n]  ubar [batch][U][d]  w [batch][nbranch]
  *   p [batch][bdim][m]       sol [batch][nv]   (full primal vector, reference layout) */

@@ -228,13 +228,16 @@ def _max_step(C, lam, d):
 
 
 def _line_search(C, lam, ds, dz, tau, dtau, kap, dkap):
+    """Largest step keeping (lam + a ds, lam + a dz, tau, kappa) interior, capped at STEPMAX.
+
+    Unlike a STEPMIN floor, a step is never forced past the boundary: a (near) zero step is
+    reported to the caller, which treats it as a numerical stall."""
     a = min(_max_step(C, lam, ds), _max_step(C, lam, dz))
     if dtau < 0:
         a = min(a, -tau / dtau)
     if dkap < 0:
         a = min(a, -kap / dkap)
-    a = min(a, STEPMAX)
-    return max(a, STEPMIN) if np.isfinite(a) else STEPMAX
+    return max(0.0, min(a, STEPMAX))
 
 
 class KKT:
@@ -373,6 +376,7 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
     resz0 = max(1.0, np.linalg.norm(h))
     info = dict(exitFlag=ECOS_MAXIT, iter=0)
     best = None          # (score, iterate, stats)
+    stall = 0
 
     def pack(code, it, st, xs, ys, zs, ss, ts):
         info.update(st, exitFlag=code, iter=it)
@@ -415,6 +419,8 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
                   f"pres {pres:.2e} dres {dres:.2e} k/t {kap / tau:.2e}")
 
         def exit_check(ft, at, rt_):
+            if not (tau > 0 and kap >= 0):
+                return None
             if ((-cx > 0 or -by - hz >= -at) and pres < ft and dres < ft
                     and (gap < at or (not np.isnan(relgap) and relgap < rt_))):
                 return ECOS_OPTIMAL
@@ -427,10 +433,23 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
 
         # ECOS safeguard: remember the best iterate by its worst residual
         score = max(pres, dres, relgap if not np.isnan(relgap) else np.inf)
+        # stall counter: only in the end game (best iterate already meets the inaccurate
+        # tolerances), iterations that do not halve the best score
+        stall = 0 if (best is None or score < 0.5 * best[0] or best[0] > FEASTOL_INACC) else stall + 1
         if best is None or score < best[0]:
             best = (score, it, stats, x.copy(), y.copy(), z.copy(), s.copy(), tau)
 
         code = exit_check(feastol, abstol, reltol)
+        if code is None and stall >= 5:         # no progress for 5 end-game iterations
+            code2 = exit_check(FEASTOL_INACC, ABSTOL_INACC, RELTOL_INACC)
+            if code2 is not None:
+                code = code2 + ECOS_INACC_OFFSET
+            else:
+                _, bit, bst, bx_, by_, bz_, bs_, btau = best
+                ok = (bst['pres'] < FEASTOL_INACC and bst['dres'] < FEASTOL_INACC and
+                      (bst['gap'] < ABSTOL_INACC or (not np.isnan(bst['relgap']) and bst['relgap'] < RELTOL_INACC)))
+                return pack(ECOS_OPTIMAL + ECOS_INACC_OFFSET if ok else ECOS_MAXIT, it, bst,
+                            bx_, by_, bz_, bs_, btau)
         if code is None and it == maxit:
             code2 = exit_check(FEASTOL_INACC, ABSTOL_INACC, RELTOL_INACC)
             code = ECOS_MAXIT if code2 is None else code2 + ECOS_INACC_OFFSET
@@ -471,6 +490,8 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
             dsW = xi - Wdz
             dkap = (dk_c - kap * dtau) / tau
             alpha = _line_search(C, lam, dsW, Wdz, tau, dtau, kap, dkap) * GAMMA
+            if not alpha > 1e-10:
+                raise FloatingPointError("step length collapsed")
             ds = W.W(dsW)
             if verbose:
                 print(f"      a_aff {a_aff:.3f} alpha {alpha:.3f} sigma {sigma:.2e}")

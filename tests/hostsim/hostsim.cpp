@@ -103,6 +103,20 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   return 0;
 }
 
+int hs_set_warm_start(void* p, const double* uLin, const double* pprev, const double* jcons) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  for (int e = 0; e < h->batch; ++e) {
+    double* ws = h->ws.data() + L.stride * e;
+    memcpy(ws + L.uLin, uLin + (size_t)e * (P.U + 1) * P.d, sizeof(double) * (P.U + 1) * P.d);
+    memcpy(ws + L.pprev, pprev + (size_t)e * P.bdim * P.m, sizeof(double) * P.bdim * P.m);
+    ws[L.misc + MISC_JCONS] = jcons[e];
+    ws[L.misc + MISC_INIT] = 1.0;
+  }
+  return 0;
+}
+
 int hs_get_tree(void* p, double* xbar, double* ubar, double* zbar, double* w, double* pr,
                 double* sol) {
   HS* h = (HS*)p;

@@ -85,6 +85,13 @@ class HostSim:
         lib().hs_solve(self.h, _p(x), _p(z), _p(xref), _p(up), _p(xp), _p(bw), _p(J), _p(st), _p(it))
         return dict(upred=up, xpred=xp, branch_w=bw, J=J, status=st, iters=it)
 
+    def set_warm_start(self, uLin, pprev, jcons):
+        B = self.batch
+        uLin = np.ascontiguousarray(np.asarray(uLin, float).reshape(B, self.U + 1, self.desc.d))
+        pprev = np.ascontiguousarray(np.asarray(pprev, float).reshape(B, self.bdim, self.desc.m))
+        jcons = np.ascontiguousarray(np.asarray(jcons, float).reshape(B))
+        lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons))
+
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d
         out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),

@@ -1,0 +1,58 @@
+"""The C ABI library loads and exports every entry point include/bmpc.h declares (no device
+access), and the ctypes mirror matches the header's struct layout."""
+import ctypes as C
+import os
+import re
+
+from common import REPO
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "bmpc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(bmpc_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_all_header_symbols():
+    from bmpc import _lib
+    _lib.build()
+    lib = C.CDLL(_lib.SO_PATH)
+    names = header_functions()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_library_is_gfx950_code_object():
+    from bmpc import _lib
+    _lib.build()
+    blob = open(_lib.SO_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_without_device():
+    from bmpc import _lib
+    lib = _lib.load()
+    assert lib.bmpc_abi_version() == 1
+
+
+def test_desc_struct_layout_matches_header():
+    """sizeof(bmpc_plan_desc) from the header, computed by the host compiler."""
+    import subprocess
+    import tempfile
+    from bmpc import abi
+    code = ('#include <stdio.h>\n#include <stddef.h>\n#include "bmpc.h"\n'
+            'int main(){printf("%zu %zu %zu %zu\\n", sizeof(bmpc_plan_desc), offsetof(bmpc_plan_desc, Q),'
+            ' offsetof(bmpc_plan_desc, mc), sizeof(bmpc_policy));return 0;}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(code)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I" + os.path.join(REPO, "include"), c, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split()
+    size, offQ, offmc, psize = map(int, out)
+    assert size == C.sizeof(abi.PlanDesc)
+    assert offQ == abi.PlanDesc.Q.offset
+    assert offmc == abi.PlanDesc.mc.offset
+    assert psize == C.sizeof(abi.Policy)
