@@ -990,17 +990,19 @@ BMPC_HD bool kkt_coupling(const X& ex, const Ctx& C) {
   return small_lu(ex, M, ws + L.piv, ns);
 }
 
-// Solve [0 A' G'; A 0 0; G 0 -W^2] [dx; dy; dz] = [r1; r2; r3]  (one pass)
+// One pass of the W-scaled KKT system (oracle/ecos_ipm.py KKT)
+//   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
+// by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
 template <class X, int NX, int NU>
 BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const double* r2,
-                            const double* r3, double* dx, double* dy, double* dz) {
+                            const double* r3h, double* dx, double* dy, double* dzh) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
   double* ws = C.ws;
   double* tr = ws + L.k_r0;
   double* tz = ws + L.k_nv0;
-  apply_W(ex, C, 3, r3, tr);                      // W^-2 r3
-  apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-2 r3
+  apply_W(ex, C, 1, r3h, tr);                     // W^-1 r3h
+  apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-1 r3h
   for (int i = ex.lane; i < P.nv; i += ex.nlanes) tz[i] += r1[i];
   ex.sync();
   {
@@ -1045,49 +1047,59 @@ BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const d
   for (int i = ex.lane; i < ng; i += ex.nlanes) dx[gvar(P, i)] = b[i];
   for (int j = ex.lane; j < nb; j += ex.nlanes) dy[P.T * NX + j] = b[ng + j];
   ex.sync();
-  // dz = W^-2 (G dx - r3)
+  // dzh = W^-1 G dx - r3h
   apply_G<X, NX, NU>(ex, C, dx, tr);
-  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) tr[i] -= r3[i];
+  apply_W(ex, C, 1, tr, dzh);
+  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dzh[i] -= r3h[i];
   ex.sync();
-  apply_W(ex, C, 3, tr, dz);
 }
 
-// solve with iterative refinement against the unreduced KKT operator
+// Solve [0 A' G'; A 0 0; G 0 -W^2] [dx; dy; dz] = [r1; r2; r3]: W-scaled solve with
+// iterative refinement on the scaled residual (well conditioned, unlike the W^2 form whose
+// residual is dominated by the rounding of W^2 dz near the boundary).
 template <class X, int NX, int NU>
 BMPC_HD void kkt_solve(const X& ex, const Ctx& C, const double* r1, const double* r2,
                        const double* r3, double* dx, double* dy, double* dz) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
   double* ws = C.ws;
-  kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3, dx, dy, dz);
   double* e1 = ws + L.k_e1;
   double* e2 = ws + L.k_e2;
   double* e3 = ws + L.k_e3;
-  double* t3 = ws + L.k_t3;
+  double* r3h = ws + L.k_t3;
   double* cx = ws + L.k_cx;
   double* cy = ws + L.k_cy;
   double* cz = ws + L.k_cz;
-  // scale of the right-hand side
+  double* tv = ws + L.k_nv1;
+  apply_W(ex, C, 1, r3, r3h);
+  kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz);   // dz holds dzh until the end
   double sc = 0.0;
   for (int i = ex.lane; i < P.nv; i += ex.nlanes) sc = fmax(sc, fabs(r1[i]));
   for (int i = ex.lane; i < P.neq; i += ex.nlanes) sc = fmax(sc, fabs(r2[i]));
-  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) sc = fmax(sc, fabs(r3[i]));
+  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) sc = fmax(sc, fabs(r3h[i]));
   sc = ex.max(sc);
   for (int itr = 0; itr < 3; ++itr) {
+    // e1 = r1 - A'dy - G'W^-1 dzh
+    apply_W(ex, C, 1, dz, e3);
+    apply_GT<X, NX, NU>(ex, C, e3, tv);
     apply_AT<X, NX, NU>(ex, C, dy, e1);
-    apply_GT<X, NX, NU>(ex, C, dz, ws + L.k_nv1);
-    for (int i = ex.lane; i < P.nv; i += ex.nlanes) e1[i] = r1[i] - e1[i] - ws[L.k_nv1 + i];
+    for (int i = ex.lane; i < P.nv; i += ex.nlanes) e1[i] = r1[i] - e1[i] - tv[i];
+    // e2 = r2 - A dx
     apply_A<X, NX, NU>(ex, C, dx, e2);
     for (int i = ex.lane; i < P.neq; i += ex.nlanes) e2[i] = r2[i] - e2[i];
-    apply_G<X, NX, NU>(ex, C, dx, e3);
-    apply_W(ex, C, 2, dz, t3);
-    for (int i = ex.lane; i < P.nrows; i += ex.nlanes) e3[i] = r3[i] - e3[i] + t3[i];
+    // e3 = r3h - W^-1 G dx + dzh
+    apply_G<X, NX, NU>(ex, C, dx, cz);
+    apply_W(ex, C, 1, cz, e3);
+    for (int i = ex.lane; i < P.nrows; i += ex.nlanes) e3[i] = r3h[i] - e3[i] + dz[i];
     ex.sync();
     double err = 0.0;
     for (int i = ex.lane; i < P.nv; i += ex.nlanes) err = fmax(err, fabs(e1[i]));
     for (int i = ex.lane; i < P.neq; i += ex.nlanes) err = fmax(err, fabs(e2[i]));
     for (int i = ex.lane; i < P.nrows; i += ex.nlanes) err = fmax(err, fabs(e3[i]));
     err = ex.max(err);
+#ifdef BMPC_HOST_DEBUG
+    printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
+#endif
     if (!(err > 1e-14 * fmax(sc, 1.0))) break;
     kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz);
     for (int i = ex.lane; i < P.nv; i += ex.nlanes) dx[i] += cx[i];
@@ -1095,6 +1107,10 @@ BMPC_HD void kkt_solve(const X& ex, const Ctx& C, const double* r1, const double
     for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dz[i] += cz[i];
     ex.sync();
   }
+  // dz = W^-1 dzh
+  apply_W(ex, C, 1, dz, e3);
+  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dz[i] = e3[i];
+  ex.sync();
 }
 
 // ECOS bring2cone: s = r + (1 + alpha) e

@@ -16,7 +16,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-for _p in (REPO, os.path.join(REPO, "belief-planning_amd"), os.path.join(REPO, "tests")):
+for _p in (REPO, os.path.join(REPO, "belief-planning_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
@@ -56,14 +56,14 @@ def cpu_baseline(N, NB, sample, procs):
 def _worker_init():
     os.environ["OMP_NUM_THREADS"] = "1"
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
-    for _p in (REPO, os.path.join(REPO, "tests")):
+    for _p in (REPO, os.path.join(REPO, "belief-planning_amd")):
         if _p not in sys.path:
             sys.path.insert(0, _p)
 
 
 def _cpu_solve(args):
     i, N, NB = args
-    from common import seeded_batch
+    from bmpc.scenarios import seeded_batch
     from oracle.ecos_ipm import ecos_solve
     from oracle.model import HighwayModel, highway_policies
     from oracle.tree import CVaRController
@@ -106,7 +106,7 @@ def main():
     import torch
     import torch.distributed as dist
     from bmpc import plan
-    from common import highway_desc, highway_policy_rows, seeded_batch
+    from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

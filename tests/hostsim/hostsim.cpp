@@ -117,6 +117,14 @@ int hs_set_warm_start(void* p, const double* uLin, const double* pprev, const do
   return 0;
 }
 
+int hs_reset(void* p, const uint8_t* mask) {
+  HS* h = (HS*)p;
+  const Layout& L = h->hp.lay;
+  for (int e = 0; e < h->batch; ++e)
+    if (!mask || mask[e]) h->ws[L.stride * e + L.misc + MISC_INIT] = 0.0;
+  return 0;
+}
+
 int hs_get_tree(void* p, double* xbar, double* ubar, double* zbar, double* w, double* pr,
                 double* sol) {
   HS* h = (HS*)p;

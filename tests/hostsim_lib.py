@@ -92,6 +92,10 @@ class HostSim:
         jcons = np.ascontiguousarray(np.asarray(jcons, float).reshape(B))
         lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons))
 
+    def reset_mask(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        lib().hs_reset(self.h, _p(m))
+
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d
         out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),

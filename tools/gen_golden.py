@@ -136,11 +136,21 @@ def gen_highway(name, N, NB, steps, keep, out):
                  L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef0,
                  Q=param.Q, R=param.R, Fx=param.Fx, bx=np.asarray(param.bx, float).reshape(-1),
                  Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
-    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "exit", "J", "iters", "collision")}
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "exit", "J", "iters", "collision",
+                            "ws_uLin", "ws_p")}
+    bdim = sum(3 ** k for k in range(NB))
     t0 = time.time()
     for t in range(steps):
         if not env.collision:
             env.check_collision()
+        # warm start the controller carries into this solve (updatetree inputs,
+        # MPC_branch.py:1813-1823): uLin and the old p of the non-leaf branches (BFS order)
+        if mpc.uLin is None:
+            traj["ws_uLin"].append(None)
+            traj["ws_p"].append(None)
+        else:
+            traj["ws_uLin"].append(np.array(mpc.uLin, float).copy())
+            traj["ws_p"].append(np.array([np.ravel(b.p) for b in mpc.ndx if b.depth < NB], float))
         r = env.step(t)
         prob, sol, info, kw = CURRENT["captured"]
         assert kw == {"verbose": False}, kw
@@ -164,11 +174,13 @@ def gen_highway(name, N, NB, steps, keep, out):
             d_out[p + "exit"] = np.array(info["exitFlag"])
             d_out[p + "uPred"] = mpc.uPred
             d_out[p + "xPred"] = mpc.xPred
-            d_out[p + "uLin_prev"] = np.zeros(1) if t == 0 else d_out.get("_uLin_prev", np.zeros(1))
             xs, zs, us, ws = bt_arrays(mpc)
             d_out[p + "bt_x"], d_out[p + "bt_z"], d_out[p + "bt_u"], d_out[p + "bt_w"] = xs, zs, us, ws
         print(f"[{name}] t={t:3d} exit={info['exitFlag']:3d} it={info['iter']:3d} J={sol[-1]:.6f} "
               f"u0={mpc.uPred[0]} ({time.time() - t0:.0f}s)", flush=True)
+    for k in ("ws_uLin", "ws_p"):    # first solve has no warm start (inittree): NaN rows
+        shape = next(v.shape for v in traj[k] if v is not None)
+        traj[k] = [np.full(shape, np.nan) if v is None else v for v in traj[k]]
     for k, v in traj.items():
         d_out["traj_" + k] = np.array(v)
     d_out["keep"] = np.array(sorted(keep))
