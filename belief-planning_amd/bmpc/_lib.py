@@ -14,6 +14,7 @@ REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 SO_PATH = os.path.join(PKG_DIR, "libbmpc.so")
+PROF_SO_PATH = os.path.join(PKG_DIR, "libbmpc_prof.so")   # -DBMPC_PROFILE variant (tools only)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("BMPC_OFFLOAD_ARCH", "gfx950")
 
@@ -31,20 +32,23 @@ def headers():
     return hs + [os.path.join(INCLUDE, "bmpc.h")]
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile libbmpc.so for gfx950 (in-tree) if missing or stale."""
-    if not force and os.path.exists(SO_PATH):
+def build(force: bool = False, verbose: bool = False, profile: bool = False) -> str:
+    """Compile libbmpc.so (or the phase-counter variant libbmpc_prof.so) for gfx950 in-tree
+    if missing or stale."""
+    out = PROF_SO_PATH if profile else SO_PATH
+    if not force and os.path.exists(out):
         newest = max(os.path.getmtime(p) for p in sources() + headers())
-        if os.path.getmtime(SO_PATH) >= newest:
-            return SO_PATH
+        if os.path.getmtime(out) >= newest:
+            return out
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
-           "-I" + INCLUDE, "-I" + CSRC, *sources(), "-o", SO_PATH + ".tmp"]
+           *(["-DBMPC_PROFILE"] if profile else []),
+           "-I" + INCLUDE, "-I" + CSRC, *sources(), "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(SO_PATH + ".tmp", SO_PATH)
-    return SO_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 _LIB = None
@@ -63,6 +67,7 @@ _SIGS = {
     "bmpc_solve_device": (C.c_int, [C.c_void_p] + [C.c_void_p] * 10),
     "bmpc_get_tree": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
     "bmpc_get_warm_start": (C.c_int, [C.c_void_p] * 4),
+    "bmpc_get_counters": (C.c_int, [C.c_void_p] * 2),
     "bmpc_set_warm_start": (C.c_int, [C.c_void_p] * 5),
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -85,9 +90,11 @@ def load(path: str = SO_PATH):
 
 
 def lib():
+    """The product library; BMPC_LIBRARY may name another in-tree build of the same
+    sources (e.g. libbmpc_prof.so for phase counters)."""
     global _LIB
     if _LIB is None:
-        _LIB = load()
+        _LIB = load(os.environ.get("BMPC_LIBRARY", SO_PATH))
     return _LIB
 
 

@@ -112,6 +112,15 @@ class BatchPlan:
         return out
 
     # ---- timing ---------------------------------------------------------------------------
+    PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
+              "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree")
+
+    def counters(self):
+        """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build)."""
+        out = np.zeros((self.batch, 16))
+        check(lib().bmpc_get_counters(self._h, _p(out)), "bmpc_get_counters")
+        return out
+
     def enable_timing(self, on=True):
         check(lib().bmpc_enable_timing(self._h, 1 if on else 0), "bmpc_enable_timing")
 

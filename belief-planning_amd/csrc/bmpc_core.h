@@ -15,8 +15,12 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define BMPC_HD __host__ __device__ __forceinline__
+// phase-sized functions stay out of line: the IPM kernel calls them from many sites and
+// inlining them all blows the kernel past the instruction cache
+#define BMPC_FN __host__ __device__ __attribute__((noinline))
 #else
 #define BMPC_HD inline
+#define BMPC_FN inline
 #endif
 
 #include <math.h>
@@ -67,6 +71,9 @@ struct Plan {
   int rFx, rFu, rRisk, rPos, nlp, nrows;
   int ng;     // number of "global" variables (rho, sigma, mu+, mu-, J)
   int nsm;    // dense coupling system size
+  // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
+  int lds_M, lds_piv, lds_rhs, lds_red, nlds;
+  int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
   double W1[BMPC_MAX_N * BMPC_MAX_N];   // sqrtm(Q) / chol(Q)'  (MPC_branch.py:1628-1631)
   double Wu[BMPC_MAX_D * BMPC_MAX_D];   // chol(R)'             (:1633-1636)
   double QQ[BMPC_MAX_N * BMPC_MAX_N];   // W1'W1
@@ -86,16 +93,128 @@ struct Layout {
   size_t x, y, z, s, lam, x1, y1, z1, x2, y2, z2, dz, ds, rx, ry, rz, hvec, bvec;
   size_t ta, ya, ra, rb, rc, bestx;
   // KKT-solve scratch
-  size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_cx, k_cy, k_cz, k_nv1;
+  size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_cx, k_cy, k_cz, k_nv1, zeros;
   // scaling
   size_t dl, eta, wbar, vnt;
   // KKT
-  size_t hx, hu, sd, P, Kg, Luu, kff, lvec, gk, colk, colnu, Msm, piv, smrhs;
+  size_t hx, hu, sd, P, Kg, Luu, kff, lvec, gk, colk, colnu;
+  size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
   size_t stride;  // doubles per ego
 };
 
 // misc slots
 enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */ };
+
+// ------------------------------------------------------------------------------------
+// phase cycle counters: built with -DBMPC_PROFILE the device code accumulates s_memtime
+// cycles of each phase per ego (lane 0) into Layout::prof; otherwise the scopes vanish.
+// ------------------------------------------------------------------------------------
+enum {
+  PROF_TREE = 0, PROF_RESID, PROF_SCALING, PROF_FACTOR, PROF_COUPLING, PROF_KKT, PROF_TREESOLVE,
+  PROF_REFINE, PROF_STEP, PROF_INIT, PROF_TOTAL, PROF_NSOLVE, PROF_APPLYW, PROF_APPLYG, PROF_APPLYGT,
+  PROF_NTREE, PROF_COUNT = 16
+};
+#if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+struct ProfScope {
+  double* slot;
+  long long t0;
+  __device__ ProfScope(double* ws, size_t base, int id) : slot(ws + base + id), t0(__builtin_amdgcn_s_memtime()) {}
+  __device__ ~ProfScope() {
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) *slot += (double)(t1 - t0);
+  }
+};
+#define BMPC_PROF(ws, L, id) ProfScope _prof_##id((ws), (L).prof, id)
+#define BMPC_TIC(v) const long long v = __builtin_amdgcn_s_memtime()
+#define BMPC_TOC(ws, L, id, v) \
+  if (threadIdx.x == 0) (ws)[(L).prof + (id)] += (double)(__builtin_amdgcn_s_memtime() - (v))
+#define BMPC_COUNT(ws, L, id) \
+  if (threadIdx.x == 0) (ws)[(L).prof + (id)] += 1.0
+#else
+#define BMPC_PROF(ws, L, id) ((void)0)
+#define BMPC_TIC(v) ((void)0)
+#define BMPC_TOC(ws, L, id, v) ((void)0)
+#define BMPC_COUNT(ws, L, id) ((void)0)
+#endif
+
+// ------------------------------------------------------------------------------------
+// batched lane loops: every lane first evaluates ld(i) for up to UN of its indices -- all
+// loads of the batch are in flight together instead of one memory round trip per element
+// -- then commits them with st(i, v).  ld must not read what st of the same batch writes.
+// ------------------------------------------------------------------------------------
+template <int UN = 8, class Ld, class St>
+BMPC_HD void strided_batch(int first, int stride, int hi, Ld ld, St st) {
+  for (int b = first; b < hi; b += UN * stride) {
+    decltype(ld(b)) v[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int i = b + u * stride;
+      if (i < hi) v[u] = ld(i);
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int i = b + u * stride;
+      if (i < hi) st(i, v[u]);
+    }
+  }
+}
+
+template <int UN = 8, class X, class Ld, class St>
+BMPC_HD void lane_batch(const X& ex, int lo, int hi, Ld ld, St st) {
+  strided_batch<UN>(lo + ex.lane, ex.nlanes, hi, ld, st);
+}
+
+// per-lane partial reduction of f(i) over first, first+stride, ... < hi with UN
+// independent accumulators (op: 0 sum, 1 max, 2 min)
+template <int UN = 8, int OP = 0, class F>
+BMPC_HD double strided_partial(int first, int stride, int hi, F f) {
+  const double init = OP == 0 ? 0.0 : OP == 1 ? -1e300 : 1e300;
+  double acc[UN];
+#pragma unroll
+  for (int u = 0; u < UN; ++u) acc[u] = init;
+  for (int b = first; b < hi; b += UN * stride) {
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int i = b + u * stride;
+      if (i < hi) {
+        const double v = f(i);
+        acc[u] = OP == 0 ? acc[u] + v : OP == 1 ? fmax(acc[u], v) : fmin(acc[u], v);
+      }
+    }
+  }
+  double s = init;
+#pragma unroll
+  for (int u = 0; u < UN; ++u) s = OP == 0 ? s + acc[u] : OP == 1 ? fmax(s, acc[u]) : fmin(s, acc[u]);
+  return s;
+}
+
+template <int UN = 8, class X, class F>
+BMPC_HD double lane_partial(const X& ex, int lo, int hi, F f) {
+  return strided_partial<UN, 0>(lo + ex.lane, ex.nlanes, hi, f);
+}
+
+// sum over the lanes of f(i), i in [lo, hi)
+template <int UN = 8, class X, class F>
+BMPC_HD double lane_sum(const X& ex, int lo, int hi, F f) {
+  return ex.sum(strided_partial<UN, 0>(lo + ex.lane, ex.nlanes, hi, f));
+}
+
+// Cone groups: the lanes split into groups of cg lanes (a power of two); group g handles
+// cones g, g + ngrp, ... in lock-step rounds so that group reductions stay convergent.
+// f(k, gl, cg) is called once per round with k = -1 for an idle group.
+struct ConeGroups {
+  int cg, ngrp, g, gl, rounds;
+};
+template <class X>
+BMPC_HD ConeGroups cone_groups(const X& ex, int cgrp, int ncones) {
+  ConeGroups G;
+  G.cg = ex.nlanes == 1 ? 1 : cgrp;
+  G.ngrp = ex.nlanes / G.cg;
+  G.g = ex.lane / G.cg;
+  G.gl = ex.lane % G.cg;
+  G.rounds = (ncones + G.ngrp - 1) / G.ngrp;
+  return G;
+}
 
 // ------------------------------------------------------------------------------------
 // small dense helpers (row-major, compile-time sizes)
@@ -114,6 +233,22 @@ BMPC_HD void mat_store(const double (&M)[R][C], double* p) {
   for (int i = 0; i < R; ++i)
 #pragma unroll
     for (int j = 0; j < C; ++j) p[i * C + j] = M[i][j];
+}
+
+template <int R, int C>
+BMPC_HD void mat_copy(const double (&S)[R][C], double (&D)[R][C]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < C; ++j) D[i][j] = S[i][j];
+}
+
+template <int R, int C>
+BMPC_HD void mat_zero(double (&D)[R][C]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < C; ++j) D[i][j] = 0.0;
 }
 
 // in-place Cholesky of an SPD D x D matrix (lower factor in L); returns false on failure

@@ -17,11 +17,45 @@
 
 using namespace bmpc;
 
+#ifndef BMPC_WPE
+#define BMPC_WPE 4   // waves per SIMD the IPM kernel is register-limited to (4 = all 4096 egos resident)
+#endif
+
 namespace {
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
 
 struct DevExec {
   int lane;
+  double* lds;   // this wave's LDS scratch (Plan::nlds doubles; k_ipm only)
   static constexpr int nlanes = 64;
+  // task groups of 4 lanes (one DPP quad) for the tree sweeps
+  static constexpr int kTaskLanes = 4;
+  __device__ double tsum(double v) const {
+    v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+    return v;
+  }
+  template <int S>
+  __device__ double tget(double v) const { return dpp_d<S | (S << 2) | (S << 4) | (S << 6)>(v); }
+  // sum over aligned groups of g lanes (g a power of two)
+  __device__ double gsum(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ double gmax(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ double gmin(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+  }
   __device__ void sync() const { __syncthreads(); }
   __device__ double sum(double v) const {
 #pragma unroll
@@ -54,13 +88,14 @@ __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, doubl
   if (e >= batch) return;
   const Plan& P = B->P;
   const Layout& L = B->L;
-  DevExec ex{(int)threadIdx.x};
+  DevExec ex{(int)threadIdx.x, nullptr};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  BMPC_PROF(E.ws, L, PROF_TREE);
   tree_update<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
 }
 
 template <class M>
-__global__ __launch_bounds__(64) void k_ipm(const Bundle* __restrict__ B, double* __restrict__ ws,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm(const Bundle* __restrict__ B, double* __restrict__ ws,
                                             const bmpc_policy* __restrict__ pol, double* upred,
                                             double* xpred, double* bw, double* J, int32_t* status,
                                             int32_t* iters, int batch) {
@@ -68,7 +103,8 @@ __global__ __launch_bounds__(64) void k_ipm(const Bundle* __restrict__ B, double
   if (e >= batch) return;
   const Plan& P = B->P;
   const Layout& L = B->L;
-  DevExec ex{(int)threadIdx.x};
+  extern __shared__ double lds_dyn[];
+  DevExec ex{(int)threadIdx.x, lds_dyn};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_ipm<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -303,6 +339,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
+  const size_t lds_bytes = sizeof(double) * (size_t)P.nlds;
   if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[0], s));
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
@@ -313,10 +350,10 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   HIPCHECK(hipGetLastError());
   if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[1], s));
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
-    hipLaunchKernelGGL(k_ipm<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+    hipLaunchKernelGGL(k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   else
-    hipLaunchKernelGGL(k_ipm<Quadruped>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+    hipLaunchKernelGGL(k_ipm<Quadruped>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   HIPCHECK(hipGetLastError());
   if (pl->timing) {
@@ -387,6 +424,12 @@ static int gather(bmpc_plan* pl, size_t off, int count, double* host) {
   HIPCHECK(hipMemcpyAsync(host, pl->d_scratch, need * sizeof(double), hipMemcpyDeviceToHost, pl->stream));
   HIPCHECK(hipStreamSynchronize(pl->stream));
   return 0;
+}
+
+int bmpc_get_counters(bmpc_plan* pl, double* out) {
+  if (!pl || !out) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  return gather(pl, pl->hp.lay.prof, PROF_COUNT, out);
 }
 
 int bmpc_get_warm_start(bmpc_plan* pl, double* uLin, double* p, double* jcons) {

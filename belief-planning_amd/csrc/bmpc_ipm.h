@@ -36,31 +36,39 @@ struct Ctx {
   BMPC_HD double* at(size_t off) const { return ws + off; }
 };
 
+// cone-group rounds (see ConeGroups): G, and per round k / off / q of the owned cone
+#define BMPC_CONE_ROUNDS(ex, P, G)                                \
+  const ConeGroups G = cone_groups(ex, (P).cgrp, (P).ncones);     \
+  for (int rnd_ = 0; rnd_ < G.rounds; ++rnd_)
+#define BMPC_CONE_K(P, G, k, off, q)                              \
+  const int k = rnd_ * G.ngrp + G.g < (P).ncones ? rnd_ * G.ngrp + G.g : -1; \
+  const int off = k >= 0 ? (P).t.cone_off[k] : 0;                 \
+  const int q = k >= 0 ? (P).t.cone_q[k] : 0
+
 // ------------------------------------------------------------------------------------
-// reductions over one cone's rows
+// reductions over one cone's rows, by the cone group G that owns the cone (k >= 0) or as an
+// idle member (k < 0, q = 0): every lane of the wave must make the same calls.
 // ------------------------------------------------------------------------------------
 template <class X>
-BMPC_HD double cone_dot(const X& ex, const double* a, const double* b, int off, int q) {
-  double s = 0.0;
-  for (int i = ex.lane; i < q; i += ex.nlanes) s += a[off + i] * b[off + i];
-  return ex.sum(s);
+BMPC_HD double cone_dot(const X ex, const ConeGroups& G, const double* a, const double* b, int off, int q) {
+  return ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) { return a[off + i] * b[off + i]; }), G.cg);
 }
 
 // v0^2 - ||v1||^2 without squaring the dominant entry (see oracle.ecos_ipm.cone_res)
 template <class X>
-BMPC_HD double cone_res(const X& ex, const double* v, int off, int q) {
-  double amax = 0.0;
-  for (int i = 1 + ex.lane; i < q; i += ex.nlanes) amax = fmax(amax, fabs(v[off + i]));
-  amax = ex.max(amax);
-  double kidx = 1e300;
-  for (int i = 1 + ex.lane; i < q; i += ex.nlanes)
-    if (fabs(v[off + i]) == amax) kidx = fmin(kidx, (double)i);
-  kidx = ex.min(kidx);
-  double ss = 0.0;
-  for (int i = 1 + ex.lane; i < q; i += ex.nlanes)
-    if ((double)i != kidx) ss += v[off + i] * v[off + i];
-  ss = ex.sum(ss);
-  return cone_res_parts(v[off], amax, ss);
+BMPC_HD double cone_res(const X ex, const ConeGroups& G, const double* v, int off, int q) {
+  double amax = 0.0, aidx = 1e300;
+  for (int i = 1 + G.gl; i < q; i += G.cg) {
+    const double a = fabs(v[off + i]);
+    if (a > amax) amax = a, aidx = (double)i;
+  }
+  const double gm = ex.gmax(amax, G.cg);
+  const double kd = ex.gmin(amax == gm && aidx < 1e300 ? aidx : 1e300, G.cg);
+  const int kidx = kd < 1e300 ? (int)kd : -1;
+  const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
+    return i == kidx ? 0.0 : v[off + i] * v[off + i];
+  }), G.cg);
+  return q > 0 ? cone_res_parts(v[off], gm, ss) : 1.0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -73,131 +81,153 @@ BMPC_HD double fx_coef(const Ctx& C, int k, int c, int j) {
   return P.desc.Fx[(c - 1) * P.n + j];
 }
 
-// value of the cone's F1 row dotted with a primal vector zv (unboosted)
-template <int NX>
-BMPC_HD double cone_f1_dot(const Ctx& C, int k, const double* zv) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
-  const int c = t.cone_c[k];
-  double acc = 0.0;
-  if (c >= 0) {
-    const int b = t.cone_b[k], i = t.cone_i[k];
-    const int ndx = t.br_ndx[c];
-    for (int j = 0; j < P.N; ++j) {
-      const int xk = ndx + j;
-      for (int r = 0; r < NX; ++r) acc += -2.0 * C.qx[r] * zv[P.oX + xk * NX + r];
-      for (int cc = 0; cc < P.Nc; ++cc) acc += P.desc.Qslack[1] * zv[P.oS + xk * P.Nc + cc];
-    }
-    acc += zv[P.oSig + b] + zv[P.oMup + b + i] - zv[P.oMum + b + i];
-    if (t.br_child0[c] >= 0) acc += zv[P.oRho + c];
-  } else {
-    acc = -zv[P.oJ] + zv[P.oRho + 0];
-    for (int cc = 0; cc < P.Nc; ++cc) acc += P.desc.Qslack[1] * zv[P.oS + cc];
-  }
-  return acc;
-}
-
 // out(rows) = G zv, cone rows boosted
 template <class X, int NX, int NU>
-BMPC_HD void apply_G(const X& ex, const Ctx& C, const double* zv, double* out) {
+BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
   const Plan& P = *C.P;
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
   const Topo& t = P.t;
   const int Nc = P.Nc;
+  const double* dh = C.at(C.L->dh);
   // Fx rows + positivity rows
-  for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
+  struct Two { double a, b; };
+  lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     const double S = zv[P.oS + it];
     double v = -S;
     if (t.x_u[k] >= 0) {
-      for (int j = 0; j < NX; ++j) v += fx_coef(C, k, c, j) * zv[P.oX + k * NX + j];
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        const double f = c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j];
+        v += f * zv[P.oX + k * NX + j];
+      }
     }
-    out[P.rFx + it] = v;
-    out[P.rPos + it] = -S;
-  }
+    return Two{v, -S};
+  }, [&](int it, Two r) { out[P.rFx + it] = r.a; out[P.rPos + it] = r.b; });
   // Fu rows
-  for (int it = ex.lane; it < P.U * P.nFu; it += ex.nlanes) {
+  lane_batch(ex, 0, P.U * P.nFu, [&](int it) {
     const int u = it / P.nFu, r = it % P.nFu;
     double v = 0.0;
+#pragma unroll
     for (int j = 0; j < NU; ++j) v += P.desc.Fu[r * NU + j] * zv[P.oU + u * NU + j];
-    out[P.rFu + it] = v;
-  }
+    return v;
+  }, [&](int it, double v) { out[P.rFu + it] = v; });
   // risk rows: -rho, -mu+, -mu-
-  for (int it = ex.lane; it < P.bdim * (2 * P.m + 1); it += ex.nlanes) {
-    out[P.rRisk + it] = it < P.bdim ? -zv[P.oRho + it] : -zv[P.oMup + (it - P.bdim)];
-  }
-  // cones
+  lane_batch(ex, 0, P.bdim * (2 * P.m + 1), [&](int it) {
+    return it < P.bdim ? -zv[P.oRho + it] : -zv[P.oMup + (it - P.bdim)];
+  }, [&](int it, double v) { out[P.rRisk + it] = v; });
   const double* boost = C.at(C.L->boost);
-  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double f = cone_f1_dot<NX>(C, k, zv) * exp(-boost[k]);
-    out[off] = f;
-    out[off + q - 1] = -f;
-  }
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], c = t.cone_c[k];
+  const double Qs = P.desc.Qslack[1];
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const int c = k >= 0 ? t.cone_c[k] : -1;
+    // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node
+    {
+      const int ndx = c >= 0 ? t.br_ndx[c] : 0;
+      const int nn = c >= 0 ? P.N : (k >= 0 ? 1 : 0);
+      double part = strided_partial<4>(G.gl, G.cg, nn, [&](int j) {
+        double a = 0.0;
+        if (c >= 0) {
+#pragma unroll
+          for (int r2 = 0; r2 < NX; ++r2) a += -2.0 * C.qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
+        }
+        for (int cc = 0; cc < P.Nc; ++cc) a += Qs * zv[P.oS + (ndx + j) * P.Nc + cc];
+        return a;
+      });
+      const double f1 = ex.gsum(part, G.cg);
+      if (k >= 0 && G.gl == 0) {
+        double acc = f1;
+        if (c >= 0) {
+          const int b = t.cone_b[k], i = t.cone_i[k];
+          acc += zv[P.oSig + b] + zv[P.oMup + b + i] - zv[P.oMum + b + i];
+          if (t.br_child0[c] >= 0) acc += zv[P.oRho + c];
+        } else {
+          acc += -zv[P.oJ] + zv[P.oRho + 0];
+        }
+        const double f = acc * exp(-boost[k]);
+        out[off] = f;
+        out[off + q - 1] = -f;
+      }
+    }
+    // middle rows: rows are contiguous after each cone's first
     const int nxn = c >= 0 ? P.N * NX : 0;
-    const int nmid = c >= 0 ? P.N * (NX + NU) : NU;
-    for (int it = ex.lane; it < nmid; it += ex.nlanes) {
+    const int nmid = k < 0 ? 0 : c >= 0 ? P.N * (NX + NU) : NU;
+    strided_batch<4>(G.gl, G.cg, nmid, [&](int it) {
       double v = 0.0;
       if (it < nxn) {
         const int j = it / NX, r = it % NX;
         const int xk = t.br_ndx[c] + j;
-        for (int s = 0; s < NX; ++s) v += -2.0 * P.W1[r * NX + s] * zv[P.oX + xk * NX + s];
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) v += -2.0 * P.W1[r * NX + s2] * zv[P.oX + xk * NX + s2];
       } else {
         const int jj = it - nxn;
         const int j = jj / NU, r = jj % NU;
         const int uk = c >= 0 ? t.br_ndu[c] + j : 0;
-        for (int s = 0; s < NU; ++s) v += -2.0 * P.Wu[r * NU + s] * zv[P.oU + uk * NU + s];
+#pragma unroll
+        for (int s2 = 0; s2 < NU; ++s2) v += -2.0 * P.Wu[r * NU + s2] * zv[P.oU + uk * NU + s2];
       }
-      out[off + 1 + it] = v;
-    }
+      return v;
+    }, [&](int it, double v) { out[off + 1 + it] = v; });
   }
   ex.sync();
 }
 
 // out(nv) = G' r
 template <class X, int NX, int NU>
-BMPC_HD void apply_GT(const X& ex, const Ctx& C, const double* r, double* out) {
+BMPC_FN void apply_GT(const X ex, const Ctx& C, const double* r, double* out) {
   const Plan& P = *C.P;
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYGT);
   const Topo& t = P.t;
   const int Nc = P.Nc;
   const double* boost = C.at(C.L->boost);
+  const double* dh = C.at(C.L->dh);
   const double Qs = P.desc.Qslack[1];
-  // state nodes: x and S parts
+  // state nodes: x and S parts (all loads of a node first, stores after)
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
-    double ax[NX];
-    for (int j = 0; j < NX; ++j) ax[j] = 0.0;
+    double ax[NX], cx[NX], os[BMPC_MAX_FX + 1];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) ax[j] = 0.0, cx[j] = 0.0;
     const bool term = t.x_u[k] < 0;
-    for (int c = 0; c < Nc; ++c) {
-      const double rv = r[P.rFx + k * Nc + c];
-      if (!term)
-        for (int j = 0; j < NX; ++j) ax[j] += fx_coef(C, k, c, j) * rv;
-      out[P.oS + k * Nc + c] = -rv - r[P.rPos + k * Nc + c];
-    }
+    double fS = 0.0;
     const int kc = t.x_cone[k];
     if (kc >= 0) {
       const int off = t.cone_off[kc], q = t.cone_q[kc], j = t.x_conepos[k];
       const double f = (r[off] - r[off + q - 1]) * exp(-boost[kc]);
-      for (int s = 0; s < NX; ++s) {
+#pragma unroll
+      for (int s2 = 0; s2 < NX; ++s2) {
         double v = 0.0;
-        for (int rr = 0; rr < NX; ++rr) v += -2.0 * P.W1[rr * NX + s] * r[off + 1 + j * NX + rr];
-        ax[s] += v - 2.0 * C.qx[s] * f;
+#pragma unroll
+        for (int rr = 0; rr < NX; ++rr) v += -2.0 * P.W1[rr * NX + s2] * r[off + 1 + j * NX + rr];
+        cx[s2] = v - 2.0 * C.qx[s2] * f;
       }
-      for (int c = 0; c < Nc; ++c) out[P.oS + k * Nc + c] += Qs * f;
+      fS = Qs * f;
     } else if (k == 0) {  // root slack in the root cone
       const int kr = P.ncones - 1;
       const int off = t.cone_off[kr], q = t.cone_q[kr];
-      const double f = (r[off] - r[off + q - 1]) * exp(-boost[kr]);
-      for (int c = 0; c < Nc; ++c) out[P.oS + c] += Qs * f;
+      fS = Qs * (r[off] - r[off + q - 1]) * exp(-boost[kr]);
     }
-    for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = ax[j];
+    double dhk[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) dhk[j] = dh[k * NX + j];
+    for (int c = 0; c < Nc; ++c) {
+      const double rv = r[P.rFx + k * Nc + c];
+      if (!term)
+#pragma unroll
+        for (int j = 0; j < NX; ++j) ax[j] += (c == 0 ? -dhk[j] : P.desc.Fx[(c - 1) * NX + j]) * rv;
+      os[c] = -rv - r[P.rPos + k * Nc + c] + fS;
+    }
+    for (int c = 0; c < Nc; ++c) out[P.oS + k * Nc + c] = os[c];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = kc >= 0 ? ax[j] + cx[j] : ax[j];
   }
   // input nodes
   for (int u = ex.lane; u < P.U; u += ex.nlanes) {
     double au[NU];
+#pragma unroll
     for (int j = 0; j < NU; ++j) au[j] = 0.0;
     for (int rr = 0; rr < P.nFu; ++rr) {
       const double rv = r[P.rFu + u * P.nFu + rr];
+#pragma unroll
       for (int j = 0; j < NU; ++j) au[j] += P.desc.Fu[rr * NU + j] * rv;
     }
     const int kc = t.u_cone[u];
@@ -205,55 +235,75 @@ BMPC_HD void apply_GT(const X& ex, const Ctx& C, const double* r, double* out) {
       const int off = t.cone_off[kc];
       const int c = t.cone_c[kc];
       const int base = c >= 0 ? 1 + P.N * NX + (u - t.br_ndu[c]) * NU : 1;
-      for (int s = 0; s < NU; ++s) {
+#pragma unroll
+      for (int s2 = 0; s2 < NU; ++s2) {
         double v = 0.0;
-        for (int rr = 0; rr < NU; ++rr) v += -2.0 * P.Wu[rr * NU + s] * r[off + base + rr];
-        au[s] += v;
+#pragma unroll
+        for (int rr = 0; rr < NU; ++rr) v += -2.0 * P.Wu[rr * NU + s2] * r[off + base + rr];
+        au[s2] += v;
       }
     }
+#pragma unroll
     for (int j = 0; j < NU; ++j) out[P.oU + u * NU + j] = au[j];
   }
-  // globals (one lane; few entries)
-  if (ex.lane == 0) {
-    for (int i = 0; i < P.ng; ++i) out[i == P.ng - 1 ? P.oJ : P.oRho + i] = 0.0;
-    for (int b = 0; b < P.bdim; ++b) out[P.oRho + b] = -r[P.rRisk + b];
-    for (int j = 0; j < 2 * P.bdim * P.m; ++j) out[P.oMup + j] = -r[P.rRisk + P.bdim + j];
+  // globals: one lane per global variable, gathering its cone and risk-row terms
+  for (int i = ex.lane; i < P.ng; i += ex.nlanes) {
+    double v = 0.0;
+    const int gi = i == P.ng - 1 ? P.oJ : P.oRho + i;
+    if (gi < P.oSig) v = -r[P.rRisk + (gi - P.oRho)];                     // rho
+    else if (gi >= P.oMup && gi < P.oS) v = -r[P.rRisk + P.bdim + (gi - P.oMup)];   // mu+, mu-
     for (int k = 0; k < P.ncones; ++k) {
       const int off = t.cone_off[k], q = t.cone_q[k], c = t.cone_c[k];
-      const double f = (r[off] - r[off + q - 1]) * exp(-boost[k]);
+      double w = 0.0;
       if (c >= 0) {
-        const int b = t.cone_b[k], i = t.cone_i[k];
-        out[P.oSig + b] += f;
-        out[P.oMup + b + i] += f;
-        out[P.oMum + b + i] -= f;
-        if (t.br_child0[c] >= 0) out[P.oRho + c] += f;
+        const int b = t.cone_b[k], ii = t.cone_i[k];
+        if (gi == P.oSig + b) w += 1.0;
+        if (gi == P.oMup + b + ii) w += 1.0;
+        if (gi == P.oMum + b + ii) w -= 1.0;
+        if (t.br_child0[c] >= 0 && gi == P.oRho + c) w += 1.0;
       } else {
-        out[P.oJ] += -f;
-        out[P.oRho + 0] += f;
+        if (gi == P.oJ) w -= 1.0;
+        if (gi == P.oRho) w += 1.0;
       }
+      if (w != 0.0) v += w * (r[off] - r[off + q - 1]) * exp(-boost[k]);
     }
+    out[gi] = v;
   }
   ex.sync();
 }
 
 // out(neq) = A zv
 template <class X, int NX, int NU>
-BMPC_HD void apply_A(const X& ex, const Ctx& C, const double* zv, double* out) {
+BMPC_HD void apply_A(const X ex, const Ctx& C, const double* zv, double* out) {
   const Plan& P = *C.P;
   const Topo& t = P.t;
   const double* Ad = C.at(C.L->Ad);
   const double* Bd = C.at(C.L->Bd);
-  for (int k = ex.lane; k < P.T; k += ex.nlanes) {
+  struct V4 { double v[NX]; };
+  lane_batch<2>(ex, 0, P.T, [&](int k) {
     const int su = t.x_srcu[k], sx = t.x_srcx[k];
-    for (int r = 0; r < NX; ++r) {
-      double v = zv[P.oX + k * NX + r];
-      if (su >= 0) {
-        for (int s = 0; s < NX; ++s) v -= Ad[su * NX * NX + r * NX + s] * zv[P.oX + sx * NX + s];
-        for (int s = 0; s < NU; ++s) v -= Bd[su * NX * NU + r * NU + s] * zv[P.oU + su * NU + s];
+    V4 o;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) o.v[r] = zv[P.oX + k * NX + r];
+    if (su >= 0) {
+      double xs[NX], us[NU];
+#pragma unroll
+      for (int s2 = 0; s2 < NX; ++s2) xs[s2] = zv[P.oX + sx * NX + s2];
+#pragma unroll
+      for (int s2 = 0; s2 < NU; ++s2) us[s2] = zv[P.oU + su * NU + s2];
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) o.v[r] -= Ad[su * NX * NX + r * NX + s2] * xs[s2];
+#pragma unroll
+        for (int s2 = 0; s2 < NU; ++s2) o.v[r] -= Bd[su * NX * NU + r * NU + s2] * us[s2];
       }
-      out[k * NX + r] = v;
     }
-  }
+    return o;
+  }, [&](int k, const V4& o) {
+#pragma unroll
+    for (int r = 0; r < NX; ++r) out[k * NX + r] = o.v[r];
+  });
   const double* p = C.at(C.L->p);
   for (int b = ex.lane; b < P.bdim; b += ex.nlanes) {
     double v = zv[P.oRho + b] + zv[P.oSig + b];
@@ -265,54 +315,66 @@ BMPC_HD void apply_A(const X& ex, const Ctx& C, const double* zv, double* out) {
 
 // out(nv) = A' y
 template <class X, int NX, int NU>
-BMPC_HD void apply_AT(const X& ex, const Ctx& C, const double* y, double* out) {
+BMPC_HD void apply_AT(const X ex, const Ctx& C, const double* y, double* out) {
   const Plan& P = *C.P;
   const Topo& t = P.t;
   const double* Ad = C.at(C.L->Ad);
   const double* Bd = C.at(C.L->Bd);
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     double ax[NX], au[NU];
+#pragma unroll
     for (int r = 0; r < NX; ++r) ax[r] = y[k * NX + r];
+#pragma unroll
     for (int r = 0; r < NU; ++r) au[r] = 0.0;
     const int u = t.x_u[k];
     if (u >= 0) {
       double ys[NX];
+#pragma unroll
       for (int r = 0; r < NX; ++r) ys[r] = 0.0;
       for (int e = t.succ_off[k]; e < t.succ_off[k + 1]; ++e) {
         const int c = t.succ[e];
+#pragma unroll
         for (int r = 0; r < NX; ++r) ys[r] += y[c * NX + r];
       }
-      for (int s = 0; s < NX; ++s) {
+#pragma unroll
+      for (int s2 = 0; s2 < NX; ++s2) {
         double v = 0.0;
-        for (int r = 0; r < NX; ++r) v += Ad[u * NX * NX + r * NX + s] * ys[r];
-        ax[s] -= v;
+#pragma unroll
+        for (int r = 0; r < NX; ++r) v += Ad[u * NX * NX + r * NX + s2] * ys[r];
+        ax[s2] -= v;
       }
-      for (int s = 0; s < NU; ++s) {
+#pragma unroll
+      for (int s2 = 0; s2 < NU; ++s2) {
         double v = 0.0;
-        for (int r = 0; r < NX; ++r) v += Bd[u * NX * NU + r * NU + s] * ys[r];
-        au[s] -= v;
+#pragma unroll
+        for (int r = 0; r < NX; ++r) v += Bd[u * NX * NU + r * NU + s2] * ys[r];
+        au[s2] -= v;
       }
-      for (int s = 0; s < NU; ++s) out[P.oU + u * NU + s] = au[s];
+#pragma unroll
+      for (int s2 = 0; s2 < NU; ++s2) out[P.oU + u * NU + s2] = au[s2];
     }
+#pragma unroll
     for (int r = 0; r < NX; ++r) out[P.oX + k * NX + r] = ax[r];
   }
-  for (int it = ex.lane; it < P.T * P.Nc; it += ex.nlanes) out[P.oS + it] = 0.0;
+  lane_batch(ex, P.oS, P.oJ, [&](int) { return 0.0; }, [&](int i, double v) { out[i] = v; });
   const double* p = C.at(C.L->p);
-  if (ex.lane == 0) {
-    for (int i = 0; i < P.ng; ++i) out[i == P.ng - 1 ? P.oJ : P.oRho + i] = 0.0;
-    for (int b = 0; b < P.bdim; ++b) {
-      const double yb = y[P.T * NX + b];
-      out[P.oRho + b] += yb;
-      out[P.oSig + b] += yb;
-      for (int i = 0; i < P.m; ++i) out[P.oMum + b * P.m + i] += -p[b * P.m + i] / C.ralpha * yb;
+  for (int i = ex.lane; i < P.ng; i += ex.nlanes) {
+    const int gi = i == P.ng - 1 ? P.oJ : P.oRho + i;
+    double v = 0.0;
+    if (gi < P.oSig) v = y[P.T * NX + (gi - P.oRho)];
+    else if (gi < P.oMup) v = y[P.T * NX + (gi - P.oSig)];
+    else if (gi >= P.oMum && gi < P.oS) {
+      const int j = gi - P.oMum, b = j / P.m, ii = j % P.m;
+      v = -p[b * P.m + ii] / C.ralpha * y[P.T * NX + b];
     }
+    out[gi] = v;
   }
   ex.sync();
 }
 
 // h (rows) and b (eq) of this solve
 template <class X, int NX, int NU>
-BMPC_HD void build_hb(const X& ex, const Ctx& C, double* h, double* bv) {
+BMPC_HD void build_hb(const X ex, const Ctx& C, double* h, double* bv) {
   const Plan& P = *C.P;
   const Topo& t = P.t;
   const int Nc = P.Nc;
@@ -351,187 +413,293 @@ BMPC_HD void build_hb(const X& ex, const Ctx& C, double* h, double* bv) {
 }
 
 // ------------------------------------------------------------------------------------
-// Nesterov-Todd scaling
+// Nesterov-Todd scaling and the cone algebra (ECOS; oracle/ecos_ipm.py)
 // ------------------------------------------------------------------------------------
 // returns false when an iterate left its cone
 template <class X>
-BMPC_HD bool compute_scaling(const X& ex, const Ctx& C, const double* s, const double* z) {
+BMPC_FN bool compute_scaling(const X ex, const Ctx& C, const double* s, const double* z) {
+  BMPC_PROF(C.ws, *C.L, PROF_SCALING);
   const Plan& P = *C.P;
-  const Topo& t = P.t;
   double* dl = C.at(C.L->dl);
   double* lam = C.at(C.L->lam);
   double* eta = C.at(C.L->eta);
   double* wb = C.at(C.L->wbar);
   double* vn = C.at(C.L->vnt);
-  int bad = 0;
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) {
-    if (!(s[i] > 0.0 && z[i] > 0.0)) bad = 1;
-    dl[i] = sqrt(s[i] / z[i]);
-    lam[i] = sqrt(s[i] * z[i]);
-  }
-  if (ex.max((double)bad) > 0.0) return false;
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double sres = cone_res(ex, s, off, q);
-    const double zres = cone_res(ex, z, off, q);
-    if (!(sres > 0.0 && zres > 0.0)) return false;
+  struct DL { double d, l; };
+  double bad = strided_partial<8, 1>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
+    return (s[i] > 0.0 && z[i] > 0.0) ? 0.0 : 1.0;
+  });
+  lane_batch(ex, 0, P.nlp, [&](int i) { return DL{sqrt(s[i] / z[i]), sqrt(s[i] * z[i])}; },
+             [&](int i, DL v) { dl[i] = v.d; lam[i] = v.l; });
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double sres = cone_res(ex, G, s, off, q);
+    const double zres = cone_res(ex, G, z, off, q);
+    if (!(sres > 0.0 && zres > 0.0)) bad = 1.0;
     const double sn = sqrt(sres), zn = sqrt(zres);
-    const double sz = cone_dot(ex, s, z, off, q) / (sn * zn);
+    const double sz = cone_dot(ex, G, s, z, off, q) / (sn * zn);
     const double gam = sqrt((1.0 + sz) / 2.0);
-    for (int i = ex.lane; i < q; i += ex.nlanes) {
-      const double jz = i == 0 ? z[off] : -z[off + i];
-      wb[off + i] = (s[off + i] / sn + jz / zn) / (2.0 * gam);
-    }
-    ex.sync();
-    const double w0 = wb[off];
+    // wbar = (s/sn + J z/zn) / (2 gam);  v = (wbar + e0) / sqrt(2 (wbar0 + 1))
+    const double w0 = q > 0 ? (s[off] / sn + z[off] / zn) / (2.0 * gam) : 0.0;
     const double nrm = sqrt(2.0 * (w0 + 1.0));
-    for (int i = ex.lane; i < q; i += ex.nlanes) vn[off + i] = (wb[off + i] + (i == 0 ? 1.0 : 0.0)) / nrm;
-    if (ex.lane == 0) eta[k] = sqrt(sn / zn);
-    ex.sync();
     const double e = sqrt(sn / zn);
-    const double vz = cone_dot(ex, vn, z, off, q);
-    for (int i = ex.lane; i < q; i += ex.nlanes) {
+    // v'z without storing v first: v_i = (wbar_i + [i==0]) / nrm
+    const double vz = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
       const double jz = i == 0 ? z[off] : -z[off + i];
-      lam[off + i] = e * (2.0 * vn[off + i] * vz - jz);
-    }
+      const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
+      return (w + (i == 0 ? 1.0 : 0.0)) / nrm * z[off + i];
+    }), G.cg);
+    struct WV { double w, v, l; };
+    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+      const double jz = i == 0 ? z[off] : -z[off + i];
+      const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
+      const double v = (w + (i == 0 ? 1.0 : 0.0)) / nrm;
+      return WV{w, v, e * (2.0 * v * vz - jz)};
+    }, [&](int i, WV r) { wb[off + i] = r.w; vn[off + i] = r.v; lam[off + i] = r.l; });
+    if (k >= 0 && G.gl == 0) eta[k] = e;
   }
+  bad = ex.max(bad);
   ex.sync();
-  return true;
+  return bad == 0.0;
 }
 
 // identity scaling for the initial point
 template <class X>
-BMPC_HD void identity_scaling(const X& ex, const Ctx& C) {
+BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
   double* dl = C.at(C.L->dl);
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) dl[i] = 1.0;
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    for (int i = ex.lane; i < q; i += ex.nlanes) {
-      C.ws[C.L->wbar + off + i] = i == 0 ? 1.0 : 0.0;
-      C.ws[C.L->vnt + off + i] = i == 0 ? 1.0 : 0.0;
-    }
+  double* wb = C.at(C.L->wbar);
+  double* vn = C.at(C.L->vnt);
+  lane_batch(ex, 0, P.nlp, [&](int) { return 1.0; }, [&](int i, double v) { dl[i] = v; });
+  const int c0 = P.nlp;
+  lane_batch(ex, c0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { wb[i] = v; vn[i] = v; });
+  ex.sync();
+  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
+    wb[P.t.cone_off[k]] = 1.0;
+    vn[P.t.cone_off[k]] = 1.0;
+    C.ws[C.L->eta + k] = 1.0;
   }
-  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) C.ws[C.L->eta + k] = 1.0;
   ex.sync();
 }
 
 // mode 0: W v, 1: W^-1 v, 2: W^2 v, 3: W^-2 v   (W symmetric NT scaling)
 template <class X>
-BMPC_HD void apply_W(const X& ex, const Ctx& C, int mode, const double* in, double* out) {
+BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const double* in, double* out) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
   const double* dl = C.at(C.L->dl);
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) {
+  lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
-    out[i] = mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
-  }
+    return mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
+  }, [&](int i, double v) { out[i] = v; });
   const double* eta = C.at(C.L->eta);
-  const double* wb = C.at(C.L->wbar);
-  const double* vn = C.at(C.L->vnt);
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double e = eta[k];
-    // W = e (2 v v' - J); W^-1 = (2 Jv Jv' - J)/e; W^2 = e^2 (2 wb wb' - J); W^-2 = (2 Jwb Jwb' - J)/e^2
-    const double* a = (mode == 0 || mode == 1) ? vn : wb;
-    const bool jconj = (mode == 1 || mode == 3);
-    double part = 0.0;
-    for (int i = ex.lane; i < q; i += ex.nlanes) {
-      const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
-      part += ai * in[off + i];
-    }
-    const double dot = ex.sum(part);
+  // W = e (2 v v' - J); W^-1 = (2 Jv Jv' - J)/e; W^2 = e^2 (2 wb wb' - J); W^-2 = (2 Jwb Jwb' - J)/e^2
+  const double* a = C.at((mode == 0 || mode == 1) ? C.L->vnt : C.L->wbar);
+  const bool jconj = (mode == 1 || mode == 3);
+  constexpr int UC = 8;   // cone rows per lane held in registers between the two passes
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double e = k >= 0 ? eta[k] : 1.0;
     const double sc = mode == 0 ? e : mode == 1 ? 1.0 / e : mode == 2 ? e * e : 1.0 / (e * e);
-    for (int i = ex.lane; i < q; i += ex.nlanes) {
-      const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
-      const double jv = i == 0 ? in[off] : -in[off + i];
-      out[off + i] = sc * (2.0 * ai * dot - jv);
+    const double in0 = q > 0 ? in[off] : 0.0;
+    if (q <= UC * G.cg) {   // one pass: the cone's rows stay in registers
+      double av[UC], iv[UC];
+      double part = 0.0;
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = G.gl + uu * G.cg;
+        av[uu] = i < q ? ((jconj && i > 0) ? -a[off + i] : a[off + i]) : 0.0;
+        iv[uu] = i < q ? in[off + i] : 0.0;
+        part += av[uu] * iv[uu];
+      }
+      const double dot = ex.gsum(part, G.cg);
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = G.gl + uu * G.cg;
+        if (i < q) out[off + i] = sc * (2.0 * av[uu] * dot - (i == 0 ? in0 : -iv[uu]));
+      }
+    } else {                // long cones: dot pass, then write pass
+      const double dot = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
+        const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
+        return ai * in[off + i];
+      }), G.cg);
+      strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+        const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
+        const double jv = i == 0 ? in0 : -in[off + i];
+        return sc * (2.0 * ai * dot - jv);
+      }, [&](int i, double v) { out[off + i] = v; });
     }
-    ex.sync();
   }
   ex.sync();
 }
 
 // Jordan product out = u o v
 template <class X>
-BMPC_HD void jprod(const X& ex, const Ctx& C, const double* u, const double* v, double* out) {
+BMPC_HD void jprod(const X ex, const Ctx& C, const double* u, const double* v, double* out) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) out[i] = u[i] * v[i];
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double dot = cone_dot(ex, u, v, off, q);
-    const double u0 = u[off], v0 = v[off];
-    ex.sync();
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) out[off + i] = u0 * v[off + i] + v0 * u[off + i];
-    if (ex.lane == 0) out[off] = dot;
-    ex.sync();
+  lane_batch(ex, 0, P.nlp, [&](int i) { return u[i] * v[i]; }, [&](int i, double r) { out[i] = r; });
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double dot = cone_dot(ex, G, u, v, off, q);
+    const double u0 = q > 0 ? u[off] : 0.0, v0 = q > 0 ? v[off] : 0.0;
+    strided_batch<4>(G.gl, G.cg, q, [&](int i) { return i == 0 ? dot : u0 * v[off + i] + v0 * u[off + i]; },
+                     [&](int i, double r) { out[off + i] = r; });
   }
   ex.sync();
 }
 
 // out = lam \ v  (lam o out = v)
 template <class X>
-BMPC_HD void jdiv(const X& ex, const Ctx& C, const double* lam, const double* v, double* out) {
+BMPC_HD void jdiv(const X ex, const Ctx& C, const double* lam, const double* v, double* out) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) out[i] = v[i] / lam[i];
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double rho = cone_res(ex, lam, off, q);
-    double part = 0.0;
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) part += lam[off + i] * v[off + i];
-    const double lv = ex.sum(part);
-    const double l0 = lam[off];
-    const double x0 = (l0 * v[off] - lv) / rho;
-    ex.sync();
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) out[off + i] = (v[off + i] - x0 * lam[off + i]) / l0;
-    if (ex.lane == 0) out[off] = x0;
-    ex.sync();
+  lane_batch(ex, 0, P.nlp, [&](int i) { return v[i] / lam[i]; }, [&](int i, double r) { out[i] = r; });
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double rho = cone_res(ex, G, lam, off, q);
+    const double lv = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * v[off + i]; }),
+                              G.cg);
+    const double l0 = q > 0 ? lam[off] : 1.0;
+    const double x0 = q > 0 ? (l0 * v[off] - lv) / rho : 0.0;
+    strided_batch<4>(G.gl, G.cg, q, [&](int i) { return i == 0 ? x0 : (v[off + i] - x0 * lam[off + i]) / l0; },
+                     [&](int i, double r) { out[off + i] = r; });
   }
   ex.sync();
 }
 
 // largest alpha with lam + alpha d in the cone (ECOS lineSearch for one direction)
 template <class X>
-BMPC_HD double max_step(const X& ex, const Ctx& C, const double* lam, const double* d) {
+BMPC_FN double max_step(const X ex, const Ctx& C, const double* lam, const double* d) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
-  double a = 1e300;
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes)
-    if (d[i] < 0.0) a = fmin(a, -lam[i] / d[i]);
-  a = ex.min(a);
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    const double ln2 = cone_res(ex, lam, off, q);
-    if (!(ln2 > 0.0)) return 0.0;
+  double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
+    return d[i] < 0.0 ? -lam[i] / d[i] : 1e300;
+  });
+  double bad = 0.0;
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double ln2 = cone_res(ex, G, lam, off, q);
+    if (!(ln2 > 0.0)) bad = 1.0;
     const double ln = sqrt(ln2);
-    double part = 0.0;
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) part += lam[off + i] * d[off + i];
-    const double ld = ex.sum(part);
-    const double lb0 = lam[off] / ln;
-    const double rho0 = (lam[off] * d[off] - ld) / ln;
-    const double fac = (rho0 + d[off]) / (lb0 + 1.0);
-    double ss = 0.0;
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) {
+    const double ld = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
+                              G.cg);
+    const double lb0 = q > 0 ? lam[off] / ln : 0.0;
+    const double rho0 = q > 0 ? (lam[off] * d[off] - ld) / ln : 0.0;
+    const double fac = q > 0 ? (rho0 + d[off]) / (lb0 + 1.0) : 0.0;
+    const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
       const double r1 = d[off + i] - fac * lam[off + i] / ln;
-      ss += r1 * r1;
-    }
-    ss = ex.sum(ss);
+      return r1 * r1;
+    }), G.cg);
     const double tt = sqrt(ss) - rho0;
-    if (tt > 0.0) a = fmin(a, ln / tt);
+    if (k >= 0 && tt > 0.0) a = fmin(a, ln / tt);
   }
-  return a;
+  a = ex.min(a);
+  return ex.max(bad) > 0.0 ? 0.0 : a;
+}
+
+// branches of depth dep are contiguous in BFS order: sum_{i<dep} m^i .. + m^dep
+BMPC_HD int branch_count(const Plan& P, int dep) {
+  int c = 1;
+  for (int i = 0; i < dep; ++i) c *= P.m;
+  return c;
+}
+BMPC_HD int branch_start(const Plan& P, int dep) {
+  int s = 0, c = 1;
+  for (int i = 0; i < dep; ++i) s += c, c *= P.m;
+  return s;
+}
+
+// one Riccati step at a node with input: P = hx + A'Pb A - Qux' Quu^-1 Qux,
+// Quu = hu + B'Pb B (Cholesky stored), K = -Quu^-1 Qux (stored).  Pout receives P.
+template <int NX, int NU>
+BMPC_HD bool riccati_step(const double* hx, const double* hu, const double* Ap, const double* Bp,
+                          const double (&Pb)[NX][NX], double (&Pk)[NX][NX], double* Luu_out, double* K_out) {
+  double A[NX][NX], B[NX][NU], M[NX][NX];
+  mat_load(Pk, hx);
+  mat_load(A, Ap);
+  mat_load(B, Bp);
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < NX; ++r) v += Pb[i][r] * A[r][j];
+      M[i][j] = v;
+    }
+  double Qux[NU][NX], Quu[NU][NU];
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < NX; ++r) v += A[r][i] * M[r][j];
+      Pk[i][j] += v;
+    }
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < NX; ++r) v += B[r][i] * M[r][j];
+      Qux[i][j] = v;
+    }
+  mat_load(Quu, hu);
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+        double pb = 0.0;
+#pragma unroll
+        for (int c = 0; c < NX; ++c) pb += Pb[r][c] * B[c][j];
+        v += B[r][i] * pb;
+      }
+      Quu[i][j] += v;
+    }
+  const bool ok = chol<NU>(Quu);
+  mat_store(Quu, Luu_out);
+  double K[NU][NX];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    double col[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
+    chol_solve<NU>(Quu, col);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) K[i][j] = col[i];
+  }
+  mat_store(K, K_out);
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < NU; ++r) v += Qux[r][i] * K[r][j];
+      Pk[i][j] += v;
+    }
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int j = i + 1; j < NX; ++j) {
+      const double a = 0.5 * (Pk[i][j] + Pk[j][i]);
+      Pk[i][j] = a;
+      Pk[j][i] = a;
+    }
+  return ok;
 }
 
 // ------------------------------------------------------------------------------------
 // KKT factorisation
 // ------------------------------------------------------------------------------------
 template <class X, int NX, int NU>
-BMPC_HD bool kkt_factor(const X& ex, const Ctx& C) {
+BMPC_FN bool kkt_factor(const X ex, const Ctx& C) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_FACTOR);
   const Topo& t = P.t;
   const int Nc = P.Nc;
   double* ws = C.ws;
@@ -631,213 +799,353 @@ BMPC_HD bool kkt_factor(const X& ex, const Ctx& C) {
     }
   }
   ex.sync();
-  // ---- tree Riccati factorisation (leaves -> root) ---------------------------------------
+  // ---- tree Riccati factorisation (leaves -> root), one lane per branch --------------------
+  // The cost-to-go P runs backward along each branch in registers; only at a branch end are
+  // the children's first-node P read back (written by the previous depth phase).
   const double* Ad = ws + L.Ad;
   const double* Bd = ws + L.Bd;
-  int bad = 0;
-  for (int lv = P.nlevels - 1; lv >= 0; --lv) {
-    for (int e = t.lvl_off[lv] + ex.lane; e < t.lvl_off[lv + 1]; e += ex.nlanes) {
-      const int k = t.lvl_nodes[e];
-      double Pk[NX][NX];
-      mat_load(Pk, ws + L.hx + k * NX * NX);
-      const int u = t.x_u[k];
-      if (u >= 0) {
-        double Pb[NX][NX], A[NX][NX], B[NX][NU], M[NX][NX];
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NX; ++j) Pb[i][j] = 0.0;
-        for (int sidx = t.succ_off[k]; sidx < t.succ_off[k + 1]; ++sidx) {
-          const double* Pc = ws + L.P + t.succ[sidx] * NX * NX;
-          for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Pb[i][j] += Pc[i * NX + j];
-        }
-        mat_load(A, Ad + u * NX * NX);
-        mat_load(B, Bd + u * NX * NU);
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NX; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NX; ++r) v += Pb[i][r] * A[r][j];
-            M[i][j] = v;
-          }
-        double Qux[NU][NX], Quu[NU][NU], PB[NX][NU];
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NX; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NX; ++r) v += A[r][i] * M[r][j];
-            Pk[i][j] += v;
-          }
-        for (int i = 0; i < NU; ++i)
-          for (int j = 0; j < NX; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NX; ++r) v += B[r][i] * M[r][j];
-            Qux[i][j] = v;
-          }
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NU; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NX; ++r) v += Pb[i][r] * B[r][j];
-            PB[i][j] = v;
-          }
-        mat_load(Quu, ws + L.hu + u * NU * NU);
-        for (int i = 0; i < NU; ++i)
-          for (int j = 0; j < NU; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NX; ++r) v += B[r][i] * PB[r][j];
-            Quu[i][j] += v;
-          }
-        if (!chol<NU>(Quu)) bad = 1;
-        mat_store(Quu, ws + L.Luu + u * NU * NU);
-        double K[NU][NX];
-        for (int j = 0; j < NX; ++j) {
-          double col[NU];
-          for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
-          chol_solve<NU>(Quu, col);
-          for (int i = 0; i < NU; ++i) K[i][j] = col[i];
-        }
-        mat_store(K, ws + L.Kg + u * NU * NX);
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NX; ++j) {
-            double v = 0.0;
-            for (int r = 0; r < NU; ++r) v += Qux[r][i] * K[r][j];
-            Pk[i][j] += v;
-          }
-        for (int i = 0; i < NX; ++i)
-          for (int j = i + 1; j < NX; ++j) {
-            const double a = 0.5 * (Pk[i][j] + Pk[j][i]);
-            Pk[i][j] = a;
-            Pk[j][i] = a;
-          }
+  double bad = 0.0;
+  for (int dep = P.NB; dep >= 0; --dep) {
+    const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
+    for (int bi = ex.lane; bi < nbd; bi += ex.nlanes) {
+      const int b = b0 + bi;
+      const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
+      const bool leaf = dep == P.NB;
+      double Pn[NX][NX];
+      if (leaf) {   // terminal node: P = hx
+        mat_load(Pn, ws + L.hx + (ndx + len) * NX * NX);
+        mat_store(Pn, ws + L.P + (ndx + len) * NX * NX);
       }
-      mat_store(Pk, ws + L.P + k * NX * NX);
+      for (int j = len - 1; j >= 0; --j) {
+        const int k = ndx + j, u = ndu + j;
+        double Pb[NX][NX];
+        if (j < len - 1 || leaf) {
+          mat_copy(Pn, Pb);
+        } else {
+          mat_zero(Pb);
+          const int c0 = t.br_child0[b];
+          for (int i = 0; i < P.m; ++i) {
+            const double* Pc = ws + L.P + t.br_ndx[c0 + i] * NX * NX;
+#pragma unroll
+            for (int r = 0; r < NX; ++r)
+#pragma unroll
+              for (int c = 0; c < NX; ++c) Pb[r][c] += Pc[r * NX + c];
+          }
+        }
+        if (!riccati_step<NX, NU>(ws + L.hx + k * NX * NX, ws + L.hu + u * NU * NU, Ad + u * NX * NX,
+                                  Bd + u * NX * NU, Pb, Pn, ws + L.Luu + u * NU * NU, ws + L.Kg + u * NU * NX))
+          bad = 1.0;
+        mat_store(Pn, ws + L.P + k * NX * NX);
+      }
     }
     ex.sync();
   }
-  return ex.max((double)bad) == 0.0;
+  return ex.max(bad) == 0.0;
+}
+
+// all NX entries of a row-distributed vector (lane gl holds rows gl*RX .. gl*RX+RX-1)
+template <int NX, int RX, int W, class X, int S = 0>
+BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[NX]) {
+  if constexpr (S < W) {
+#pragma unroll
+    for (int r = 0; r < RX; ++r)
+      if (S * RX + r < NX) full[S * RX + r] = ex.template tget<S>(mine[r]);
+    task_gather<NX, RX, W, X, S + 1>(ex, mine, full);
+  }
 }
 
 // Tree solve of  [H_t A_dyn'; A_dyn 0] [v; nu] = [r; e]  for nr right-hand sides.
-// rhs r_i lives in z-space (x, u, S parts at P.oX/oU/oS), e_i in eq-space (first T*n rows,
-// NULL = 0).  Solutions go to out_i (z-space tree parts) and nu_i (eq-space, NULL skips).
+// rhs r_i lives in z-space (x, u, S parts at P.oX/oU/oS), e_i in eq-space (first T*n rows;
+// pass Layout::zeros for none).  Solutions go to out_i (z-space tree parts) and nu_i
+// (eq-space, NULL skips).
+// Mapping: one task per (branch, rhs), run by a group of W = X::kTaskLanes lanes (a DPP
+// quad on the GPU); lane gl of the group owns state rows gl*RX .. gl*RX+RX-1 and the slack
+// rows c = gl, gl+W, ...  The backward affine term l and the forward state x are carried
+// in registers along the branch; branches of one depth run in parallel, depths in sequence.
 template <class X, int NX, int NU>
-BMPC_HD void tree_solve(const X& ex, const Ctx& C, int nr, const double* const* r,
+BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r,
                         const double* const* e, double* const* out, double* const* nu) {
+  constexpr int W = X::kTaskLanes;
+  constexpr int RX = (NX + W - 1) / W;
+  constexpr int MC = BMPC_MAX_FX + 1;
+  constexpr int RC = (MC + W - 1) / W;     // slack rows per lane (upper bound)
   const Plan& P = *C.P;
   const Layout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_TREESOLVE);
+  BMPC_COUNT(C.ws, L, PROF_NTREE);
   const Topo& t = P.t;
   const int Nc = P.Nc;
   double* ws = C.ws;
-  const double* Ad = ws + L.Ad;
-  const double* Bd = ws + L.Bd;
   double* lv_ = ws + L.lvec;   // [nr][T][NX]
   double* kf_ = ws + L.kff;    // [nr][U][NU]
   const size_t lstr = (size_t)P.T * NX, kstr = (size_t)P.U * NU;
-  // backward sweep
-  for (int lv = P.nlevels - 1; lv >= 0; --lv) {
-    const int nlv = t.lvl_off[lv + 1] - t.lvl_off[lv];
-    for (int it = ex.lane; it < nlv * nr; it += ex.nlanes) {
-      const int k = t.lvl_nodes[t.lvl_off[lv] + it / nr], ri = it % nr;
+  const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
+  // slack-row coefficient f_c[j] (c = 0: -dh_k; c >= 1: Fx[c-1])
+  auto fxc = [&](int c, int j, const double* dhk) { return c == 0 ? -dhk[j] : P.desc.Fx[(c - 1) * NX + j]; };
+
+  // ---- backward sweep (leaves -> root) --------------------------------------------------
+  for (int dep = P.NB; dep >= 0; --dep) {
+    const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
+    const int ntask = nbd * nr;
+    const int rounds = (ntask + ngrp - 1) / ngrp;
+    for (int rd = 0; rd < rounds; ++rd) {
+      const int task = rd * ngrp + grp;
+      if (task >= ntask) continue;       // whole group idle together
+      const int b = b0 + task / nr, ri = task % nr;
       const double* rr = r[ri];
+      const double* ee = e[ri];
       double* lvec = lv_ + ri * lstr;
-      double qx[NX];
-      for (int j = 0; j < NX; ++j) qx[j] = -rr[P.oX + k * NX + j];
-      const bool term = t.x_u[k] < 0;
-      if (!term) {  // slack elimination: rx_eff = rx + sum_c df f_c rS_c / sd_c
-        for (int c = 0; c < Nc; ++c) {
-          const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
-          const double a = df * rr[P.oS + k * Nc + c] / sd;
-          for (int j = 0; j < NX; ++j) qx[j] -= fx_coef(C, k, c, j) * a;
+      double* kf = kf_ + ri * kstr;
+      const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
+      const bool leaf = dep == P.NB;
+      const int c0 = t.br_child0[b];
+      double l[RX];
+      if (leaf) {   // terminal node: l = -r_x (no input, no slack elimination)
+        const int tn = ndx + len;
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q;
+          l[q] = i < NX ? -rr[P.oX + tn * NX + i] : 0.0;
+          if (i < NX) lvec[tn * NX + i] = l[q];
         }
       }
-      if (!term) {
-        const int u = t.x_u[k];
-        double g[NX];
-        for (int j = 0; j < NX; ++j) g[j] = 0.0;
-        for (int sidx = t.succ_off[k]; sidx < t.succ_off[k + 1]; ++sidx) {
-          const int c = t.succ[sidx];
-          const double* Pc = ws + L.P + c * NX * NX;
-          const double* lc = lvec + c * NX;
-          for (int i = 0; i < NX; ++i) {
-            double v = lc[i];
-            if (e[ri])
-              for (int j = 0; j < NX; ++j) v += Pc[i * NX + j] * e[ri][c * NX + j];
-            g[i] += v;
+      for (int jn = len - 1; jn >= 0; --jn) {
+        const int k = ndx + jn, u = ndu + jn;
+        // ---- loads (independent of the recursion) ----
+        double rx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU], dhk[NX];
+        double rS[RC], sdv[RC], dfv[RC];
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+          rx[q] = rr[P.oX + k * NX + i];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Acol[q][j] = ws[L.Ad + u * NX * NX + j * NX + i];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) Brow[q][m] = ws[L.Bd + u * NX * NU + i * NU + m];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) Kcol[q][m] = ws[L.Kg + u * NU * NX + m * NX + i];
+        }
+        mat_load(Lu, ws + L.Luu + u * NU * NU);
+#pragma unroll
+        for (int m = 0; m < NU; ++m) ru[m] = rr[P.oU + u * NU + m];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) dhk[j] = ws[L.dh + k * NX + j];
+#pragma unroll
+        for (int q = 0; q < RC; ++q) {
+          const int c = gl + q * W < Nc ? gl + q * W : Nc - 1;
+          rS[q] = rr[P.oS + k * Nc + c];
+          sdv[q] = ws[L.sd + (k * Nc + c) * 2];
+          dfv[q] = ws[L.sd + (k * Nc + c) * 2 + 1];
+        }
+        // ---- g = sum over successors of (l_c + P_c e_c), own rows ----
+        double g[RX];
+        if (jn < len - 1 || leaf) {
+          double ec[NX];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) ec[j] = ee[(k + 1) * NX + j];
+#pragma unroll
+          for (int q = 0; q < RX; ++q) {
+            const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+            double v = l[q];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) v += ws[L.P + (k + 1) * NX * NX + i * NX + j] * ec[j];
+            g[q] = v;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < RX; ++q) g[q] = 0.0;
+          for (int ci = 0; ci < P.m; ++ci) {
+            const int c = t.br_ndx[c0 + ci];
+            double ec[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) ec[j] = ee[c * NX + j];
+#pragma unroll
+            for (int q = 0; q < RX; ++q) {
+              const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+              double v = lvec[c * NX + i];
+#pragma unroll
+              for (int j = 0; j < NX; ++j) v += ws[L.P + c * NX * NX + i * NX + j] * ec[j];
+              g[q] += v;
+            }
           }
         }
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+          if (gl * RX + q >= NX) g[q] = 0.0;
+        double gfull[NX];
+        task_gather<NX, RX, W>(ex, g, gfull);
+        // ---- qu = -ru + B'g ----
         double qu[NU];
-        for (int i = 0; i < NU; ++i) {
-          double v = -rr[P.oU + u * NU + i];
-          for (int j = 0; j < NX; ++j) v += Bd[u * NX * NU + j * NU + i] * g[j];
-          qu[i] = v;
-        }
-        for (int i = 0; i < NX; ++i) {
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
           double v = 0.0;
-          for (int j = 0; j < NX; ++j) v += Ad[u * NX * NX + j * NX + i] * g[j];
-          qx[i] += v;
+#pragma unroll
+          for (int q = 0; q < RX; ++q) v += Brow[q][m] * g[q];
+          qu[m] = -ru[m] + ex.tsum(v);
         }
-        double Lu[NU][NU], kf[NU];
-        mat_load(Lu, ws + L.Luu + u * NU * NU);
-        for (int i = 0; i < NU; ++i) kf[i] = -qu[i];
-        chol_solve<NU>(Lu, kf);
-        const double* K = ws + L.Kg + u * NU * NX;
-        for (int i = 0; i < NX; ++i) {
-          double v = 0.0;
-          for (int j = 0; j < NU; ++j) v += K[j * NX + i] * qu[j];
-          qx[i] += v;
+        // ---- slack elimination sum_c f_c a_c (lane owns slack rows c = gl + q W) ----
+        double sl[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) sl[j] = 0.0;
+#pragma unroll
+        for (int q = 0; q < RC; ++q) {
+          const int c = gl + q * W;
+          if (c < Nc) {
+            const double a = dfv[q] * rS[q] / sdv[q];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) sl[j] += fxc(c, j, dhk) * a;
+          }
         }
-        for (int i = 0; i < NU; ++i) kf_[ri * kstr + u * NU + i] = kf[i];
+        double slf[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) slf[j] = ex.tsum(sl[j]);
+        // ---- l_k = -rx - sl + A'g + K'qu ;  kf = -Quu^-1 qu ----
+        double kfv[NU];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) kfv[m] = -qu[m];
+        chol_solve<NU>(Lu, kfv);
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q;
+          double v = -rx[q] - slf[i < NX ? i : NX - 1];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) v += Acol[q][j] * gfull[j];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) v += Kcol[q][m] * qu[m];
+          l[q] = v;
+          if (i < NX) lvec[k * NX + i] = v;
+        }
+        if (gl == 0)
+#pragma unroll
+          for (int m = 0; m < NU; ++m) kf[u * NU + m] = kfv[m];
       }
-      for (int j = 0; j < NX; ++j) lvec[k * NX + j] = qx[j];
     }
     ex.sync();
   }
-  // forward sweep
+
+  // ---- forward sweep (root -> leaves) -----------------------------------------------------
   for (int it = ex.lane; it < nr; it += ex.nlanes) {
-    for (int j = 0; j < NX; ++j) out[it][P.oX + j] = e[it] ? e[it][j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) out[it][P.oX + j] = e[it][j];
   }
   ex.sync();
-  for (int lv = 0; lv < P.nlevels; ++lv) {
-    const int nlv = t.lvl_off[lv + 1] - t.lvl_off[lv];
-    for (int it = ex.lane; it < nlv * nr; it += ex.nlanes) {
-      const int k = t.lvl_nodes[t.lvl_off[lv] + it / nr], ri = it % nr;
+  for (int dep = 0; dep <= P.NB; ++dep) {
+    const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
+    const int ntask = nbd * nr;
+    const int rounds = (ntask + ngrp - 1) / ngrp;
+    for (int rd = 0; rd < rounds; ++rd) {
+      const int task = rd * ngrp + grp;
+      if (task >= ntask) continue;
+      const int b = b0 + task / nr, ri = task % nr;
       double* o = out[ri];
       const double* rr = r[ri];
-      double xk[NX];
-      for (int j = 0; j < NX; ++j) xk[j] = o[P.oX + k * NX + j];
-      const double* Pk = ws + L.P + k * NX * NX;
-      const double* lk = lv_ + ri * lstr + k * NX;
-      if (nu[ri])
-        for (int i = 0; i < NX; ++i) {
-          double v = lk[i];
-          for (int j = 0; j < NX; ++j) v += Pk[i * NX + j] * xk[j];
-          nu[ri][k * NX + i] = -v;
+      const double* ee = e[ri];
+      double* nn = nu[ri];
+      const double* lvec = lv_ + ri * lstr;
+      const double* kf = kf_ + ri * kstr;
+      const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
+      const bool leaf = dep == P.NB;
+      const int c0 = t.br_child0[b];
+      double xk[NX];      // full state (every lane of the group holds all of it)
+#pragma unroll
+      for (int j = 0; j < NX; ++j) xk[j] = o[P.oX + ndx * NX + j];   // written by the parent group
+      const int nnodes = leaf ? len + 1 : len;
+      for (int jn = 0; jn < nnodes; ++jn) {
+        const int k = ndx + jn;
+        const bool term = jn == len;
+        const int u = term ? ndu + len - 1 : ndu + jn;    // (terminal: input loads unused)
+        // ---- loads ----
+        double Prow[RX][NX], lk[RX], Arow[RX][NX], Brow[RX][NU], Kcol[RX][NU], kfu[NU], en[RX], dhk[NX];
+        double rS[RC], sdv[RC], dfv[RC];
+        const int kn = (jn < len - 1 || leaf) ? k + 1 : t.br_ndx[c0 >= 0 ? c0 : 0];
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Prow[q][j] = ws[L.P + k * NX * NX + i * NX + j];
+          lk[q] = lvec[k * NX + i];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Arow[q][j] = ws[L.Ad + u * NX * NX + i * NX + j];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) Brow[q][m] = ws[L.Bd + u * NX * NU + i * NU + m];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) Kcol[q][m] = ws[L.Kg + u * NU * NX + m * NX + i];
+          en[q] = ee[(term ? k : kn) * NX + i];
         }
-      const bool term = t.x_u[k] < 0;
-      for (int c = 0; c < Nc; ++c) {  // slack recovery
-        const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
-        double fx = 0.0;
-        if (!term)
-          for (int j = 0; j < NX; ++j) fx += fx_coef(C, k, c, j) * xk[j];
-        o[P.oS + k * Nc + c] = (rr[P.oS + k * Nc + c] + df * fx) / sd;
-      }
-      if (!term) {
-        const int u = t.x_u[k];
-        const double* K = ws + L.Kg + u * NU * NX;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) kfu[m] = kf[u * NU + m];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) dhk[j] = ws[L.dh + k * NX + j];
+#pragma unroll
+        for (int q = 0; q < RC; ++q) {
+          const int c = gl + q * W < Nc ? gl + q * W : Nc - 1;
+          rS[q] = rr[P.oS + k * Nc + c];
+          sdv[q] = ws[L.sd + (k * Nc + c) * 2];
+          dfv[q] = ws[L.sd + (k * Nc + c) * 2 + 1];
+        }
+        // ---- nu_k = -(l_k + P_k x_k), own rows ----
+        if (nn)
+#pragma unroll
+          for (int q = 0; q < RX; ++q) {
+            const int i = gl * RX + q;
+            double v = lk[q];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) v += Prow[q][j] * xk[j];
+            if (i < NX) nn[k * NX + i] = -v;
+          }
+        // ---- slack recovery, own slack rows ----
+#pragma unroll
+        for (int q = 0; q < RC; ++q) {
+          const int c = gl + q * W;
+          if (c < Nc) {
+            double fx = 0.0;
+            if (!term)
+#pragma unroll
+              for (int j = 0; j < NX; ++j) fx += fxc(c, j, dhk) * xk[j];
+            o[P.oS + k * Nc + c] = (rS[q] + dfv[q] * fx) / sdv[q];
+          }
+        }
+        if (term) break;
+        // ---- u = kf + K x ----
         double uk[NU];
-        for (int i = 0; i < NU; ++i) {
-          double v = kf_[ri * kstr + u * NU + i];
-          for (int j = 0; j < NX; ++j) v += K[i * NX + j] * xk[j];
-          uk[i] = v;
-          o[P.oU + u * NU + i] = v;
-        }
-        double xp[NX];
-        for (int i = 0; i < NX; ++i) {
+#pragma unroll
+        for (int m = 0; m < NU; ++m) {
           double v = 0.0;
-          for (int j = 0; j < NX; ++j) v += Ad[u * NX * NX + i * NX + j] * xk[j];
-          for (int j = 0; j < NU; ++j) v += Bd[u * NX * NU + i * NU + j] * uk[j];
-          xp[i] = v;
+#pragma unroll
+          for (int q = 0; q < RX; ++q) v += gl * RX + q < NX ? Kcol[q][m] * xk[gl * RX + q < NX ? gl * RX + q : 0] : 0.0;
+          uk[m] = kfu[m] + ex.tsum(v);
         }
-        for (int sidx = t.succ_off[k]; sidx < t.succ_off[k + 1]; ++sidx) {
-          const int c = t.succ[sidx];
-          for (int i = 0; i < NX; ++i) o[P.oX + c * NX + i] = xp[i] + (e[ri] ? e[ri][c * NX + i] : 0.0);
+        if (gl == 0)
+#pragma unroll
+          for (int m = 0; m < NU; ++m) o[P.oU + u * NU + m] = uk[m];
+        // ---- x_next = A x + B u (+ e), own rows, then gather ----
+        double xn[RX];
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          double v = 0.0;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) v += Arow[q][j] * xk[j];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) v += Brow[q][m] * uk[m];
+          xn[q] = v;
+        }
+        if (jn < len - 1 || leaf) {
+#pragma unroll
+          for (int q = 0; q < RX; ++q) {
+            const int i = gl * RX + q;
+            xn[q] += en[q];
+            if (i < NX) o[P.oX + (k + 1) * NX + i] = xn[q];
+          }
+          task_gather<NX, RX, W>(ex, xn, xk);
+        } else {
+          for (int ci = 0; ci < P.m; ++ci) {
+            const int c = t.br_ndx[c0 + ci];
+#pragma unroll
+            for (int q = 0; q < RX; ++q) {
+              const int i = gl * RX + q;
+              if (i < NX) o[P.oX + c * NX + i] = xn[q] + ee[c * NX + i];
+            }
+          }
         }
       }
     }
@@ -845,9 +1153,9 @@ BMPC_HD void tree_solve(const X& ex, const Ctx& C, int nr, const double* const* 
   }
 }
 
-// dense LU with partial pivoting of the coupling system (row-major nsm x nsm)
+// dense LU with partial pivoting of the coupling system (row-major n x n, in LDS)
 template <class X>
-BMPC_HD bool small_lu(const X& ex, double* M, double* piv, int n) {
+BMPC_FN bool small_lu(const X ex, double* M, double* piv, int n) {
   for (int k = 0; k < n; ++k) {
     double best = -1.0, bi = 1e300;
     for (int i = k + ex.lane; i < n; i += ex.nlanes) {
@@ -855,10 +1163,7 @@ BMPC_HD bool small_lu(const X& ex, double* M, double* piv, int n) {
       if (a > best || (a == best && i < bi)) best = a, bi = (double)i;
     }
     const double amax = ex.max(best);
-    double cand = 1e300;
-    for (int i = k + ex.lane; i < n; i += ex.nlanes)
-      if (fabs(M[i * n + k]) == amax) cand = fmin(cand, (double)i);
-    const int p = (int)ex.min(cand);
+    const int p = (int)ex.min(best == amax ? bi : 1e300);
     if (!(amax > 0.0)) return false;
     ex.sync();
     if (p != k)
@@ -880,9 +1185,10 @@ BMPC_HD bool small_lu(const X& ex, double* M, double* piv, int n) {
   return true;
 }
 
+// solve with the LU above; b in LDS, column-oriented substitution (one step per row)
 template <class X>
-BMPC_HD void small_lu_solve(const X& ex, const double* M, const double* piv, double* b, int n) {
-  if (ex.lane == 0) {
+BMPC_HD void small_lu_solve(const X ex, const double* M, const double* piv, double* b, int n) {
+  if (ex.lane == 0)
     for (int k = 0; k < n; ++k) {
       const int p = (int)piv[k];
       if (p != k) {
@@ -891,18 +1197,19 @@ BMPC_HD void small_lu_solve(const X& ex, const double* M, const double* piv, dou
         b[p] = tmp;
       }
     }
-    for (int i = 0; i < n; ++i) {
-      double v = b[i];
-      for (int j = 0; j < i; ++j) v -= M[i * n + j] * b[j];
-      b[i] = v;
-    }
-    for (int i = n - 1; i >= 0; --i) {
-      double v = b[i];
-      for (int j = i + 1; j < n; ++j) v -= M[i * n + j] * b[j];
-      b[i] = v / M[i * n + i];
-    }
-  }
   ex.sync();
+  for (int i = 0; i < n; ++i) {          // L (unit diagonal)
+    const double bi = b[i];
+    for (int j = i + 1 + ex.lane; j < n; j += ex.nlanes) b[j] -= M[j * n + i] * bi;
+    ex.sync();
+  }
+  for (int i = n - 1; i >= 0; --i) {     // U
+    const double bi = b[i] / M[i * n + i];
+    for (int j = ex.lane; j < i; j += ex.nlanes) b[j] -= M[j * n + i] * bi;
+    ex.sync();
+    if (ex.lane == 0) b[i] = bi;
+    ex.sync();
+  }
 }
 
 // global variable index -> position in the primal vector
@@ -910,9 +1217,10 @@ BMPC_HD int gvar(const Plan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + 
 
 // Woodbury columns, coupling matrix and its LU; returns false on breakdown
 template <class X, int NX, int NU>
-BMPC_HD bool kkt_coupling(const X& ex, const Ctx& C) {
+BMPC_FN bool kkt_coupling(const X ex, const Ctx& C) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_COUPLING);
   double* ws = C.ws;
   const int nc = P.ncones;
   const double* rr[32];
@@ -921,80 +1229,73 @@ BMPC_HD bool kkt_coupling(const X& ex, const Ctx& C) {
   double* nn[32];
   for (int k = 0; k < nc; ++k) {
     rr[k] = ws + L.gk + (size_t)k * P.nv;
-    ee[k] = nullptr;
+    ee[k] = ws + L.zeros;
     oo[k] = ws + L.colk + (size_t)k * P.nv;
     nn[k] = ws + L.colnu + (size_t)k * P.neq;
   }
   tree_solve<X, NX, NU>(ex, C, nc, rr, ee, oo, nn);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
-  double* M = ws + L.Msm;
+  double* M = ex.lds + P.lds_M;
   const double* eta = ws + L.eta;
   const double* dl = ws + L.dl;
   const double* p = ws + L.p;
   const int ntree = P.oRho;    // x and u parts are [0, oRho); S part [oS, oJ)
+  for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
+  ex.sync();
   // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables
   for (int it = 0; it < nc * nc; ++it) {
     const int k = it / nc, j = it % nc;
     const double* g = ws + L.gk + (size_t)k * P.nv;
     const double* col = ws + L.colk + (size_t)j * P.nv;
-    double s = 0.0;
-    for (int i = ex.lane; i < ntree; i += ex.nlanes) s += g[i] * col[i];
-    for (int i = P.oS + ex.lane; i < P.oJ; i += ex.nlanes) s += g[i] * col[i];
+    double s = lane_partial(ex, 0, ntree, [&](int i) { return g[i] * col[i]; }) +
+               lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * col[i]; });
     s = ex.sum(s);
     if (ex.lane == 0) {
       const double ck = 2.0 / (eta[k] * eta[k]);
       M[(ng + nb + k) * ns + ng + nb + j] = ck * s + (k == j ? 1.0 : 0.0);
     }
   }
-  if (ex.lane == 0) {
-    for (int i = 0; i < ng + nb; ++i)
-      for (int j = 0; j < ns; ++j) M[i * ns + j] = 0.0;
-    for (int k = 0; k < nc; ++k)
-      for (int j = 0; j < ng + nb; ++j) M[(ng + nb + k) * ns + j] = 0.0;
-    // H_gg diagonal: LP rows -rho, -mu+, -mu-
-    for (int b = 0; b < nb; ++b) {
-      const double w = dl[P.rRisk + b];
-      M[b * ns + b] = 1.0 / (w * w);
-    }
-    for (int j = 0; j < 2 * nb * P.m; ++j) {
-      const double w = dl[P.rRisk + nb + j];
-      const int gi = 2 * nb + j;
-      M[gi * ns + gi] = 1.0 / (w * w);
-    }
-    // CVaR equality rows and their transpose
-    for (int b = 0; b < nb; ++b) {
-      const int row = ng + b;
-      M[row * ns + b] = 1.0;
-      M[b * ns + row] = 1.0;
-      M[row * ns + nb + b] = 1.0;
-      M[(nb + b) * ns + row] = 1.0;
-      for (int i = 0; i < P.m; ++i) {
-        const int gi = 2 * nb + nb * P.m + b * P.m + i;
-        const double a = -p[b * P.m + i] / C.ralpha;
-        M[row * ns + gi] = a;
-        M[gi * ns + row] = a;
-      }
-    }
-    // cone coupling with the globals
-    for (int k = 0; k < nc; ++k) {
-      const double* g = ws + L.gk + (size_t)k * P.nv;
-      const double ck = 2.0 / (eta[k] * eta[k]);
-      for (int i = 0; i < ng; ++i) {
-        const double gv = g[gvar(P, i)];
-        M[i * ns + ng + nb + k] = gv;
-        M[(ng + nb + k) * ns + i] = -ck * gv;
-      }
+  // H_gg diagonal: LP rows -rho, -mu+, -mu-
+  for (int b = ex.lane; b < nb; b += ex.nlanes) {
+    const double w = dl[P.rRisk + b];
+    M[b * ns + b] = 1.0 / (w * w);
+  }
+  for (int j = ex.lane; j < 2 * nb * P.m; j += ex.nlanes) {
+    const double w = dl[P.rRisk + nb + j];
+    const int gi = 2 * nb + j;
+    M[gi * ns + gi] = 1.0 / (w * w);
+  }
+  // CVaR equality rows and their transpose
+  for (int b = ex.lane; b < nb; b += ex.nlanes) {
+    const int row = ng + b;
+    M[row * ns + b] = 1.0;
+    M[b * ns + row] = 1.0;
+    M[row * ns + nb + b] = 1.0;
+    M[(nb + b) * ns + row] = 1.0;
+    for (int i = 0; i < P.m; ++i) {
+      const int gi = 2 * nb + nb * P.m + b * P.m + i;
+      const double a = -p[b * P.m + i] / C.ralpha;
+      M[row * ns + gi] = a;
+      M[gi * ns + row] = a;
     }
   }
+  // cone coupling with the globals
+  for (int it = ex.lane; it < nc * ng; it += ex.nlanes) {
+    const int k = it / ng, i = it % ng;
+    const double gv = ws[L.gk + (size_t)k * P.nv + gvar(P, i)];
+    const double ck = 2.0 / (eta[k] * eta[k]);
+    M[i * ns + ng + nb + k] = gv;
+    M[(ng + nb + k) * ns + i] = -ck * gv;
+  }
   ex.sync();
-  return small_lu(ex, M, ws + L.piv, ns);
+  return small_lu(ex, M, ex.lds + P.lds_piv, ns);
 }
 
 // One pass of the W-scaled KKT system (oracle/ecos_ipm.py KKT)
 //   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
 template <class X, int NX, int NU>
-BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const double* r2,
+BMPC_FN void kkt_solve_once(const X ex, const Ctx& C, const double* r1, const double* r2,
                             const double* r3h, double* dx, double* dy, double* dzh) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
@@ -1003,7 +1304,7 @@ BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const d
   double* tz = ws + L.k_nv0;
   apply_W(ex, C, 1, r3h, tr);                     // W^-1 r3h
   apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-1 r3h
-  for (int i = ex.lane; i < P.nv; i += ex.nlanes) tz[i] += r1[i];
+  lane_batch<16>(ex, 0, P.nv, [&](int i) { return tz[i] + r1[i]; }, [&](int i, double v) { tz[i] = v; });
   ex.sync();
   {
     const double* rr[1] = {tz};
@@ -1013,44 +1314,42 @@ BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const d
     tree_solve<X, NX, NU>(ex, C, 1, rr, ee, oo, nn);
   }
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
-  double* b = ws + L.smrhs;
+  double* b = ex.lds + P.lds_rhs;
   const double* eta = ws + L.eta;
   for (int k = 0; k < nc; ++k) {
     const double* g = ws + L.gk + (size_t)k * P.nv;
-    double s = 0.0;
-    for (int i = ex.lane; i < P.oRho; i += ex.nlanes) s += g[i] * dx[i];
-    for (int i = P.oS + ex.lane; i < P.oJ; i += ex.nlanes) s += g[i] * dx[i];
-    s = ex.sum(s);
-    if (ex.lane == 0) b[ng + nb + k] = 2.0 / (eta[k] * eta[k]) * s;
+    const double sk = ex.sum(lane_partial(ex, 0, P.oRho, [&](int i) { return g[i] * dx[i]; }) +
+                             lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * dx[i]; }));
+    if (ex.lane == 0) b[ng + nb + k] = 2.0 / (eta[k] * eta[k]) * sk;
   }
-  if (ex.lane == 0) {
-    for (int i = 0; i < ng; ++i) b[i] = tz[gvar(P, i)];
-    for (int j = 0; j < nb; ++j) b[ng + j] = r2[P.T * NX + j];
-  }
+  for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
-  small_lu_solve(ex, ws + L.Msm, ws + L.piv, b, ns);
-  for (int i = ex.lane; i < P.oRho; i += ex.nlanes) {
+  small_lu_solve(ex, ex.lds + P.lds_M, ex.lds + P.lds_piv, b, ns);
+  const double* bc = b + ng + nb;
+  const double* colk = ws + L.colk;
+  const double* colnu = ws + L.colnu;
+  auto woodbury_x = [&](int i) {
     double v = dx[i];
-    for (int k = 0; k < nc; ++k) v -= b[ng + nb + k] * ws[L.colk + (size_t)k * P.nv + i];
-    dx[i] = v;
-  }
-  for (int i = P.oS + ex.lane; i < P.oJ; i += ex.nlanes) {
-    double v = dx[i];
-    for (int k = 0; k < nc; ++k) v -= b[ng + nb + k] * ws[L.colk + (size_t)k * P.nv + i];
-    dx[i] = v;
-  }
-  for (int i = ex.lane; i < P.T * NX; i += ex.nlanes) {
+    for (int k = 0; k < nc; ++k) v -= bc[k] * colk[(size_t)k * P.nv + i];
+    return v;
+  };
+  auto put_x = [&](int i, double v) { dx[i] = v; };
+  lane_batch(ex, 0, P.oRho, woodbury_x, put_x);
+  lane_batch(ex, P.oS, P.oJ, woodbury_x, put_x);
+  lane_batch(ex, 0, P.T * NX, [&](int i) {
     double v = dy[i];
-    for (int k = 0; k < nc; ++k) v -= b[ng + nb + k] * ws[L.colnu + (size_t)k * P.neq + i];
-    dy[i] = v;
+    for (int k = 0; k < nc; ++k) v -= bc[k] * colnu[(size_t)k * P.neq + i];
+    return v;
+  }, [&](int i, double v) { dy[i] = v; });
+  for (int i = ex.lane; i < ng + nb; i += ex.nlanes) {
+    if (i < ng) dx[gvar(P, i)] = b[i];
+    else dy[P.T * NX + i - ng] = b[i];
   }
-  for (int i = ex.lane; i < ng; i += ex.nlanes) dx[gvar(P, i)] = b[i];
-  for (int j = ex.lane; j < nb; j += ex.nlanes) dy[P.T * NX + j] = b[ng + j];
   ex.sync();
   // dzh = W^-1 G dx - r3h
   apply_G<X, NX, NU>(ex, C, dx, tr);
   apply_W(ex, C, 1, tr, dzh);
-  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dzh[i] -= r3h[i];
+  lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dzh[i] - r3h[i]; }, [&](int i, double v) { dzh[i] = v; });
   ex.sync();
 }
 
@@ -1058,10 +1357,11 @@ BMPC_HD void kkt_solve_once(const X& ex, const Ctx& C, const double* r1, const d
 // iterative refinement on the scaled residual (well conditioned, unlike the W^2 form whose
 // residual is dominated by the rounding of W^2 dz near the boundary).
 template <class X, int NX, int NU>
-BMPC_HD void kkt_solve(const X& ex, const Ctx& C, const double* r1, const double* r2,
+BMPC_FN void kkt_solve(const X ex, const Ctx& C, const double* r1, const double* r2,
                        const double* r3, double* dx, double* dy, double* dz) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_KKT);
   double* ws = C.ws;
   double* e1 = ws + L.k_e1;
   double* e2 = ws + L.k_e2;
@@ -1072,79 +1372,75 @@ BMPC_HD void kkt_solve(const X& ex, const Ctx& C, const double* r1, const double
   double* cz = ws + L.k_cz;
   double* tv = ws + L.k_nv1;
   apply_W(ex, C, 1, r3, r3h);
+  BMPC_COUNT(ws, L, PROF_NSOLVE);
   kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz);   // dz holds dzh until the end
-  double sc = 0.0;
-  for (int i = ex.lane; i < P.nv; i += ex.nlanes) sc = fmax(sc, fabs(r1[i]));
-  for (int i = ex.lane; i < P.neq; i += ex.nlanes) sc = fmax(sc, fabs(r2[i]));
-  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) sc = fmax(sc, fabs(r3h[i]));
-  sc = ex.max(sc);
+  const double sc = ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
+                                     strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
+                                strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
   for (int itr = 0; itr < 3; ++itr) {
+#if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+    ProfScope _pr(C.ws, L.prof, PROF_REFINE);
+#endif
     // e1 = r1 - A'dy - G'W^-1 dzh
     apply_W(ex, C, 1, dz, e3);
     apply_GT<X, NX, NU>(ex, C, e3, tv);
     apply_AT<X, NX, NU>(ex, C, dy, e1);
-    for (int i = ex.lane; i < P.nv; i += ex.nlanes) e1[i] = r1[i] - e1[i] - tv[i];
+    lane_batch<16>(ex, 0, P.nv, [&](int i) { return r1[i] - e1[i] - tv[i]; }, [&](int i, double v) { e1[i] = v; });
     // e2 = r2 - A dx
     apply_A<X, NX, NU>(ex, C, dx, e2);
-    for (int i = ex.lane; i < P.neq; i += ex.nlanes) e2[i] = r2[i] - e2[i];
+    lane_batch(ex, 0, P.neq, [&](int i) { return r2[i] - e2[i]; }, [&](int i, double v) { e2[i] = v; });
     // e3 = r3h - W^-1 G dx + dzh
     apply_G<X, NX, NU>(ex, C, dx, cz);
     apply_W(ex, C, 1, cz, e3);
-    for (int i = ex.lane; i < P.nrows; i += ex.nlanes) e3[i] = r3h[i] - e3[i] + dz[i];
+    lane_batch<16>(ex, 0, P.nrows, [&](int i) { return r3h[i] - e3[i] + dz[i]; }, [&](int i, double v) { e3[i] = v; });
     ex.sync();
-    double err = 0.0;
-    for (int i = ex.lane; i < P.nv; i += ex.nlanes) err = fmax(err, fabs(e1[i]));
-    for (int i = ex.lane; i < P.neq; i += ex.nlanes) err = fmax(err, fabs(e2[i]));
-    for (int i = ex.lane; i < P.nrows; i += ex.nlanes) err = fmax(err, fabs(e3[i]));
-    err = ex.max(err);
+    const double err = ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(e1[i]); }),
+                                        strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(e2[i]); })),
+                                   strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(e3[i]); })));
 #ifdef BMPC_HOST_DEBUG
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
     if (!(err > 1e-14 * fmax(sc, 1.0))) break;
     kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz);
-    for (int i = ex.lane; i < P.nv; i += ex.nlanes) dx[i] += cx[i];
-    for (int i = ex.lane; i < P.neq; i += ex.nlanes) dy[i] += cy[i];
-    for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dz[i] += cz[i];
+    lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
+    lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });
+    lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[i] + cz[i]; }, [&](int i, double v) { dz[i] = v; });
     ex.sync();
   }
   // dz = W^-1 dzh
   apply_W(ex, C, 1, dz, e3);
-  for (int i = ex.lane; i < P.nrows; i += ex.nlanes) dz[i] = e3[i];
+  lane_batch<16>(ex, 0, P.nrows, [&](int i) { return e3[i]; }, [&](int i, double v) { dz[i] = v; });
   ex.sync();
 }
 
 // ECOS bring2cone: s = r + (1 + alpha) e
 template <class X>
-BMPC_HD void bring2cone(const X& ex, const Ctx& C, const double* r, double* s) {
+BMPC_HD void bring2cone(const X ex, const Ctx& C, const double* r, double* s) {
   const Plan& P = *C.P;
-  const Topo& t = P.t;
   double alpha = -0.99;
-  double mn = 1e300;
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) mn = fmin(mn, r[i]);
-  mn = -ex.min(mn);
+  const double mn = -ex.min(strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) { return r[i]; }));
   if (P.nlp > 0 && mn >= 0.0 && mn > alpha) alpha = mn;
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    double ss = 0.0;
-    for (int i = 1 + ex.lane; i < q; i += ex.nlanes) ss += r[off + i] * r[off + i];
-    ss = ex.sum(ss);
-    const double cres = r[off] - sqrt(ss);
-    if (cres <= 0.0 && -cres > alpha) alpha = -cres;
+  {
+    double worst = -1e300;   // max over cones of -(r0 - ||r1||) where r0 - ||r1|| <= 0
+    BMPC_CONE_ROUNDS(ex, P, G) {
+      BMPC_CONE_K(P, G, k, off, q);
+      const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return r[off + i] * r[off + i]; }),
+                                G.cg);
+      const double cres = q > 0 ? r[off] - sqrt(ss) : 1.0;
+      if (cres <= 0.0) worst = fmax(worst, -cres);
+    }
+    worst = ex.max(worst);
+    if (worst > alpha) alpha = worst;
   }
+  lane_batch<16>(ex, 0, P.nrows, [&](int i) { return r[i]; }, [&](int i, double v) { s[i] = i < P.nlp ? v + 1.0 + alpha : v; });
   ex.sync();
-  for (int i = ex.lane; i < P.nlp; i += ex.nlanes) s[i] = r[i] + 1.0 + alpha;
-  for (int k = 0; k < P.ncones; ++k) {
-    const int off = t.cone_off[k], q = t.cone_q[k];
-    for (int i = ex.lane; i < q; i += ex.nlanes) s[off + i] = r[off + i] + (i == 0 ? 1.0 + alpha : 0.0);
-  }
+  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) s[P.t.cone_off[k]] = r[P.t.cone_off[k]] + 1.0 + alpha;
   ex.sync();
 }
 
 template <class X>
-BMPC_HD double vdot(const X& ex, const double* a, const double* b, int n) {
-  double s = 0.0;
-  for (int i = ex.lane; i < n; i += ex.nlanes) s += a[i] * b[i];
-  return ex.sum(s);
+BMPC_HD double vdot(const X ex, const double* a, const double* b, int n) {
+  return lane_sum(ex, 0, n, [&](int i) { return a[i] * b[i]; });
 }
 
 struct IpmResult {
@@ -1157,7 +1453,7 @@ struct IpmResult {
 // the HSDE interior-point loop (ECOS algorithm; oracle/ecos_ipm.py is its CPU restatement)
 // ------------------------------------------------------------------------------------
 template <class X, int NX, int NU>
-BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
+BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   const Plan& P = *C.P;
   const Layout& L = *C.L;
   double* ws = C.ws;
@@ -1188,6 +1484,8 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
   const double feastol = P.desc.feastol, abstol = P.desc.abstol, reltol = P.desc.reltol;
   const double deg = (double)(P.nlp + P.ncones);
   IpmResult res{EXIT_MAXIT, 0, 0.0};
+  BMPC_PROF(ws, L, PROF_TOTAL);
+  BMPC_TIC(t_init);
 
   build_hb<X, NX, NU>(ex, C, hv, bv);
   // ---- initial point with W = I ----------------------------------------------------------
@@ -1196,15 +1494,15 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
     res.exit_flag = EXIT_NUMERICS;
     return res;
   }
-  for (int i = ex.lane; i < nv; i += ex.nlanes) tA[i] = 0.0;
+  lane_batch<16>(ex, 0, nv, [&](int i) { return 0.0; }, [&](int i, double v) { tA[i] = v; });
   ex.sync();
   kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x, y2, z2);
-  for (int i = ex.lane; i < nr; i += ex.nlanes) ra[i] = -z2[i];
+  lane_batch<16>(ex, 0, nr, [&](int i) { return -z2[i]; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
   bring2cone(ex, C, ra, s);
-  for (int i = ex.lane; i < nv; i += ex.nlanes) tA[i] = i == P.oJ ? -1.0 : 0.0;
-  for (int i = ex.lane; i < neq; i += ex.nlanes) ya[i] = 0.0;
-  for (int i = ex.lane; i < nr; i += ex.nlanes) ra[i] = 0.0;
+  lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
+  lane_batch(ex, 0, neq, [&](int i) { return 0.0; }, [&](int i, double v) { ya[i] = v; });
+  lane_batch<16>(ex, 0, nr, [&](int i) { return 0.0; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
   kkt_solve<X, NX, NU>(ex, C, tA, ya, ra, x2, y, z2);
   bring2cone(ex, C, z2, z);
@@ -1215,18 +1513,28 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
   double best_score = 1e300, best_tau = 1.0;
   int stall = 0;
   int best_it = 0;
+  BMPC_TOC(ws, L, PROF_INIT, t_init);
   double bs_pres = 0, bs_dres = 0, bs_relgap = 0, bs_gap = 0, bs_pcost = 0;
   bool bs_ok_cx = false;
 
   for (int it = 0; it <= P.desc.maxit; ++it) {
+#if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+    {   // probe: latency of one dependent global load under the kernel's own load
+      BMPC_TIC(t_lat);
+      const double probe = *(volatile const double*)(ws + L.bestx + ex.lane);
+      if (probe == 1.2345e300) ws[L.prof + PROF_STEP] += 0.0;
+      BMPC_TOC(ws, L, PROF_STEP, t_lat);
+    }
+#endif
+    BMPC_TIC(t_res);
     // residuals
     apply_AT<X, NX, NU>(ex, C, y, rx);
     apply_GT<X, NX, NU>(ex, C, z, tA);
-    for (int i = ex.lane; i < nv; i += ex.nlanes) rx[i] += tA[i] + (i == P.oJ ? tau : 0.0);
+    lane_batch<16>(ex, 0, nv, [&](int i) { return rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0)); }, [&](int i, double v) { rx[i] = v; });
     apply_A<X, NX, NU>(ex, C, x, ry);
-    for (int i = ex.lane; i < neq; i += ex.nlanes) ry[i] = bv[i] * tau - ry[i];
+    lane_batch(ex, 0, neq, [&](int i) { return bv[i] * tau - ry[i]; }, [&](int i, double v) { ry[i] = v; });
     apply_G<X, NX, NU>(ex, C, x, rz);
-    for (int i = ex.lane; i < nr; i += ex.nlanes) rz[i] = hv[i] * tau - rz[i] - s[i];
+    lane_batch<16>(ex, 0, nr, [&](int i) { return hv[i] * tau - rz[i] - s[i]; }, [&](int i, double v) { rz[i] = v; });
     ex.sync();
     const double cx = x[P.oJ];
     const double by = vdot(ex, bv, y, neq), hz = vdot(ex, hv, z, nr);
@@ -1244,10 +1552,11 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
     const double nrz = sqrt(vdot(ex, rz, rz, nr)) / fmax(resz0 + nx + ns, 1.0);
     const double pres = fmax(nry, nrz) / tau;
     const double dres = sqrt(vdot(ex, rx, rx, nv)) / fmax(resx0 + ny + nz, 1.0) / tau;
+    BMPC_TOC(ws, L, PROF_RESID, t_res);
     // infeasibility certificates (only evaluated when their preconditions hold)
     double pinfres = -1.0, dinfres = -1.0;
     if ((hz + by) / fmax(ny + nz, 1.0) < -reltol) {
-      for (int i = ex.lane; i < nv; i += ex.nlanes) ra[i] = rx[i] - (i == P.oJ ? tau : 0.0);
+      lane_batch<16>(ex, 0, nv, [&](int i) { return rx[i] - (i == P.oJ ? tau : 0.0); }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
       pinfres = sqrt(vdot(ex, ra, ra, nv)) / fmax(ny + nz, 1.0);
     }
@@ -1255,7 +1564,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       apply_A<X, NX, NU>(ex, C, x, rb);
       const double a1 = sqrt(vdot(ex, rb, rb, neq)) / fmax(nx, 1.0);
       apply_G<X, NX, NU>(ex, C, x, ra);
-      for (int i = ex.lane; i < nr; i += ex.nlanes) ra[i] += s[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return ra[i] + (s[i]); }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
       const double a2 = sqrt(vdot(ex, ra, ra, nr)) / fmax(nx + ns, 1.0);
       dinfres = fmax(a1, a2);
@@ -1281,7 +1590,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       best_tau = tau;
       bs_pres = pres, bs_dres = dres, bs_relgap = relgap, bs_gap = gap, bs_pcost = pcost;
       bs_ok_cx = (-cx > 0.0 || -by - hz >= -5e-5);
-      for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.bestx + i] = x[i];
+      lane_batch<16>(ex, 0, nv, [&](int i) { return x[i]; }, [&](int i, double v) { ws[L.bestx + i] = v; });
       ex.sync();
     }
 #ifdef BMPC_HOST_DEBUG
@@ -1295,7 +1604,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       else if (best_score < 1e300) {
         const bool inacc = bs_ok_cx && bs_pres < 1e-4 && bs_dres < 1e-4 &&
                            (bs_gap < 5e-5 || (bs_relgap >= 0.0 && bs_relgap < 5e-5));
-        for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.sol + i] = ws[L.bestx + i] / best_tau;
+        lane_batch<16>(ex, 0, nv, [&](int i) { return ws[L.bestx + i] / best_tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
         ex.sync();
         res.exit_flag = inacc ? EXIT_OPTIMAL + EXIT_INACC : EXIT_MAXIT;
         res.iters = it;
@@ -1308,7 +1617,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       code = c2 == 99 ? EXIT_MAXIT : c2 + EXIT_INACC;
     }
     if (code != 99) {
-      for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.sol + i] = x[i] / tau;
+      lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] / tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
       ex.sync();
       res.exit_flag = code;
       res.iters = it;
@@ -1321,24 +1630,24 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
     double alpha = 0.0, dtau = 0.0, dkap = 0.0;
     if (ok) {
       // c vector
-      for (int i = ex.lane; i < nv; i += ex.nlanes) tA[i] = i == P.oJ ? -1.0 : 0.0;
+      lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x1, y1, z1);
       const double den = kap / tau - (x1[P.oJ] + vdot(ex, bv, y1, neq) + vdot(ex, hv, z1, nr));
       // affine: xi = -lam
-      for (int i = ex.lane; i < nr; i += ex.nlanes) ra[i] = -lam[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return -lam[i]; }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, ra, rb);                               // W xi
-      for (int i = ex.lane; i < nr; i += ex.nlanes) rb[i] = rz[i] - rb[i];
-      for (int i = ex.lane; i < nv; i += ex.nlanes) tA[i] = -rx[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return rz[i] - rb[i]; }, [&](int i, double v) { rb[i] = v; });
+      lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2);
       const double dk_aff = -kap * tau;
       const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
-      for (int i = ex.lane; i < nr; i += ex.nlanes) dz[i] = z2[i] + dtau_a * z1[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, dz, rb);                               // W dz_aff
-      for (int i = ex.lane; i < nr; i += ex.nlanes) ds[i] = ra[i] - rb[i];   // dsW_aff
+      lane_batch<16>(ex, 0, nr, [&](int i) { return ra[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff
       ex.sync();
       const double dkap_a = (dk_aff - kap * dtau_a) / tau;
       double a_aff = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
@@ -1351,26 +1660,26 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       // combined: ds_comb = -lam o lam - dsW_a o Wdz_a + sigma mu e
       jprod(ex, C, lam, lam, ra);
       jprod(ex, C, ds, rb, rc);
-      for (int i = ex.lane; i < nr; i += ex.nlanes) ra[i] = -ra[i] - rc[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return -ra[i] - rc[i]; }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
-      for (int i = ex.lane; i < P.nlp; i += ex.nlanes) ra[i] += sigma * mu;
+      lane_batch(ex, 0, P.nlp, [&](int i) { return ra[i] + (sigma * mu); }, [&](int i, double v) { ra[i] = v; });
       for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;
       ex.sync();
       jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
       apply_W(ex, C, 0, ds, rb);                               // W xi
-      for (int i = ex.lane; i < nr; i += ex.nlanes) rb[i] = eta1 * rz[i] - rb[i];
-      for (int i = ex.lane; i < nv; i += ex.nlanes) tA[i] = -eta1 * rx[i];
-      for (int i = ex.lane; i < neq; i += ex.nlanes) ya[i] = eta1 * ry[i];
+      lane_batch<16>(ex, 0, nr, [&](int i) { return eta1 * rz[i] - rb[i]; }, [&](int i, double v) { rb[i] = v; });
+      lane_batch<16>(ex, 0, nv, [&](int i) { return -eta1 * rx[i]; }, [&](int i, double v) { tA[i] = v; });
+      lane_batch(ex, 0, neq, [&](int i) { return eta1 * ry[i]; }, [&](int i, double v) { ya[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2);
       const double dk_c = -kap * tau - dtau_a * dkap_a + sigma * mu;
       dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
-      for (int i = ex.lane; i < nv; i += ex.nlanes) x2[i] += dtau * x1[i];
-      for (int i = ex.lane; i < neq; i += ex.nlanes) y2[i] += dtau * y1[i];
-      for (int i = ex.lane; i < nr; i += ex.nlanes) z2[i] += dtau * z1[i];
+      lane_batch<16>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });
+      lane_batch(ex, 0, neq, [&](int i) { return y2[i] + (dtau * y1[i]); }, [&](int i, double v) { y2[i] = v; });
+      lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, z2, rb);                               // W dz
-      for (int i = ex.lane; i < nr; i += ex.nlanes) ds[i] = ds[i] - rb[i];   // dsW
+      lane_batch<16>(ex, 0, nr, [&](int i) { return ds[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW
       ex.sync();
       dkap = (dk_c - kap * dtau) / tau;
       double a = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
@@ -1380,16 +1689,15 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
       alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
       apply_W(ex, C, 0, ds, rb);                               // ds = W dsW
       double fin = 0.0;
-      for (int i = ex.lane; i < nv; i += ex.nlanes) fin += isfinite(x2[i]) ? 0.0 : 1.0;
+      fin = strided_partial<8, 1>(ex.lane, ex.nlanes, nv, [&](int i) { return isfinite(x2[i]) ? 0.0 : 1.0; });
       fin = ex.max(fin);
       ok = fin == 0.0 && isfinite(dtau) && alpha > 1e-10;
       if (ok) {
-        for (int i = ex.lane; i < nv; i += ex.nlanes) x[i] += alpha * x2[i];
-        for (int i = ex.lane; i < neq; i += ex.nlanes) y[i] += alpha * y2[i];
-        for (int i = ex.lane; i < nr; i += ex.nlanes) {
-          z[i] += alpha * z2[i];
-          s[i] += alpha * rb[i];
-        }
+        lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
+        lane_batch(ex, 0, neq, [&](int i) { return y[i] + (alpha * y2[i]); }, [&](int i, double v) { y[i] = v; });
+        struct ZS { double z, s; };
+        lane_batch<16>(ex, 0, nr, [&](int i) { return ZS{z[i] + alpha * z2[i], s[i] + alpha * rb[i]}; },
+                   [&](int i, ZS v) { z[i] = v.z; s[i] = v.s; });
         tau += alpha * dtau;
         kap += alpha * dkap;
         ex.sync();
@@ -1398,7 +1706,7 @@ BMPC_HD IpmResult ipm_solve(const X& ex, const Ctx& C) {
     if (!ok) {   // numerical failure: ECOS backtracks to the best iterate
       const bool inacc = bs_ok_cx && bs_pres < 1e-4 && bs_dres < 1e-4 &&
                          (bs_gap < 5e-5 || (bs_relgap >= 0.0 && bs_relgap < 5e-5));
-      for (int i = ex.lane; i < nv; i += ex.nlanes) ws[L.sol + i] = ws[L.bestx + i] / best_tau;
+      lane_batch<16>(ex, 0, nv, [&](int i) { return ws[L.bestx + i] / best_tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
       ex.sync();
       res.exit_flag = inacc ? EXIT_OPTIMAL + EXIT_INACC : EXIT_NUMERICS;
       res.iters = it;

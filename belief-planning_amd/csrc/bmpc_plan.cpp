@@ -235,6 +235,13 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.nlp = P.rPos + T * P.Nc;
   P.ng = bd * (2 * m + 2) + 1;
   P.nsm = P.ng + bd + P.ncones;
+  P.lds_M = 0;
+  P.lds_piv = P.nsm * P.nsm;
+  P.lds_rhs = P.lds_piv + P.nsm;
+  P.lds_red = P.lds_rhs + P.nsm;
+  P.nlds = P.lds_red + 64;
+  P.cgrp = 64;
+  while (P.cgrp > 1 && P.cgrp * P.ncones > 64) P.cgrp >>= 1;
 
   // ---- cones (buildIneqConstr :1940-1984): children of non-leaf branches, then the root ----
   int row = P.nlp, k = 0;
@@ -360,6 +367,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.k_cy = take(neq);
   L.k_cz = take(nr);
   L.k_nv1 = take(nv);
+  L.zeros = take(neq);   // all-zero eq-space vector (tree solves without an e term)
   L.dl = take(P.nlp);
   L.eta = take(nc);
   L.wbar = take(nr);
@@ -375,9 +383,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.gk = take((size_t)nc * nv);
   L.colk = take((size_t)nc * nv);
   L.colnu = take((size_t)nc * neq);
-  L.Msm = take((size_t)P.nsm * P.nsm);
-  L.piv = take(P.nsm);
-  L.smrhs = take(P.nsm);
+  L.prof = take(PROF_COUNT);
   L.stride = o;
   return "";
 }

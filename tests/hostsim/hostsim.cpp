@@ -19,6 +19,14 @@ namespace {
 struct HostExec {
   int lane = 0;
   int nlanes = 1;
+  double* lds = nullptr;      // stands in for the wave's LDS scratch
+  static constexpr int kTaskLanes = 1;
+  double tsum(double v) const { return v; }
+  template <int S>
+  double tget(double v) const { return v; }
+  double gsum(double v, int) const { return v; }
+  double gmax(double v, int) const { return v; }
+  double gmin(double v, int) const { return v; }
   void sync() const {}
   double sum(double v) const { return v; }
   double max(double v) const { return v; }
@@ -85,6 +93,8 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   const Plan& P = h->hp.plan;
   const Layout& L = h->hp.lay;
   HostExec ex;
+  std::vector<double> lds(P.nlds);
+  ex.lds = lds.data();
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;

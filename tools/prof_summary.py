@@ -1,0 +1,64 @@
+"""Condense rocprofv3 output directories (kernel stats + PMC passes) into small files.
+
+usage: python tools/prof_summary.py OUTDIR   (OUTDIR from tools/gpu_prof.sh)
+Writes OUTDIR/summary.json and copies every *_stats.csv next to it; deletes raw traces.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def short(name):
+    for k in ("k_ipm", "k_tree", "k_gather", "k_scatter", "k_reset", "k_model"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def main(out):
+    summ = {}
+    for st in glob.glob(os.path.join(out, "stats", "**", "*kernel_stats.csv"), recursive=True):
+        shutil.copy(st, os.path.join(out, "kernel_stats.csv"))
+        summ["kernel_stats"] = [{k: r[k] for k in r} for r in rows(st)]
+    for kt in glob.glob(os.path.join(out, "stats", "**", "*kernel_trace.csv"), recursive=True):
+        dur = defaultdict(list)
+        for r in rows(kt):
+            dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        summ["kernel_durations_ns"] = {k: {"count": len(v), "avg": sum(v) / len(v), "min": min(v), "max": max(v)}
+                                       for k, v in dur.items() if k.startswith("k_")}
+    pmc = defaultdict(lambda: defaultdict(list))
+    for cc in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
+        for r in rows(cc):
+            k = short(r["Kernel_Name"])
+            if not k.startswith("k_"):
+                continue
+            pmc[k][r["Counter_Name"]].append((r.get("Dispatch_Id"), float(r["Counter_Value"])))
+    agg = {}
+    for k, cs in pmc.items():
+        agg[k] = {}
+        for c, vals in cs.items():
+            per = defaultdict(float)
+            for d, v in vals:
+                per[d] += v
+            vs = list(per.values())
+            agg[k][c] = {"dispatches": len(vs), "avg_per_dispatch": sum(vs) / len(vs)}
+    summ["pmc"] = agg
+    with open(os.path.join(out, "summary.json"), "w") as f:
+        json.dump(summ, f, indent=1)
+    for d in ("stats", "fetch", "write", "sq", "tcc"):
+        shutil.rmtree(os.path.join(out, d), ignore_errors=True)
+    print(json.dumps(summ.get("kernel_durations_ns", {}), indent=1))
+    print(json.dumps(agg, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
