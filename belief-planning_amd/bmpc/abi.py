@@ -12,7 +12,7 @@ MODEL_HIGHWAY, MODEL_QUADRUPED = 0, 1
 POL_MAINTAIN, POL_BRAKE, POL_LC, POL_MAINTAIN_TRACKV, POL_FORWARD, POL_STOP = range(6)
 
 (INFO_T, INFO_U, INFO_BDIM, INFO_NBRANCH, INFO_NV, INFO_NEQ, INFO_NROWS, INFO_NCONES,
- INFO_LP, INFO_BATCH, INFO_COUNT) = range(11)
+ INFO_LP, INFO_BATCH, INFO_WS_DOUBLES, INFO_COUNT) = range(12)
 
 
 class Policy(C.Structure):

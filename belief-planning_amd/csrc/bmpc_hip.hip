@@ -302,6 +302,7 @@ int bmpc_plan_info(const bmpc_plan* pl, int32_t* info) {
   info[BMPC_INFO_NCONES] = P.ncones;
   info[BMPC_INFO_LP] = P.nlp;
   info[BMPC_INFO_BATCH] = pl->batch;
+  info[BMPC_INFO_WS_DOUBLES] = (int32_t)pl->hp.lay.stride;
   return 0;
 }
 

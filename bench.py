@@ -108,18 +108,15 @@ def main():
     from bmpc import plan
     from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    from bmpc import distributed as D
+    rank, local, world = D.world()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    D.init("nccl", device=dev)
     B = a.batch
-    # shard: rank r owns egos [r*B, (r+1)*B) of one global seeded population
-    x, z, xref, tgt = seeded_batch(B, seed=1000 + rank) if rank else seeded_batch(B, seed=0)
+    # one global seeded population of B*world egos; rank r owns a contiguous shard
+    lo, hi = D.shard(B * world, rank, world)
+    x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(B * world, seed=0))
     desc = highway_desc(N=a.N, NB=a.NB)
     pl = plan.BatchPlan(desc, B, device=local)
     pl.set_policies(highway_policy_rows(tgt))
@@ -130,7 +127,7 @@ def main():
     Jv = torch.zeros(B, device=dev, dtype=torch.float64)
     st = torch.zeros(B, device=dev, dtype=torch.int32)
     it = torch.zeros(B, device=dev, dtype=torch.int32)
-    stats = torch.zeros(8, device=dev, dtype=torch.float64)
+    stats = torch.zeros(D.NSTAT, device=dev, dtype=torch.float64)
     stream = torch.cuda.current_stream(dev)
     dt, v0 = 0.1, 20.0
 
@@ -152,12 +149,12 @@ def main():
         tr[:, 2] = vdes
         # closed-loop statistics (Highway_sim collision rule :421-429)
         dis = torch.maximum(torch.abs(tx[:, 0] - tz[:, 0]) - 4.0, torch.abs(tx[:, 1] - tz[:, 1]) - 2.4)
-        stats[0] += Jv.sum()
-        stats[1] += (Jv * Jv).sum()
-        stats[2] += (st < 0).sum()
-        stats[3] += it.sum()
-        stats[4] += B
-        stats[5] += (dis < 0).sum()
+        stats[D.STAT_J] += Jv.sum()
+        stats[D.STAT_J2] += (Jv * Jv).sum()
+        stats[D.STAT_INFEAS] += (st < 0).sum()
+        stats[D.STAT_ITERS] += it.sum()
+        stats[D.STAT_SOLVES] += B
+        stats[D.STAT_COLL] += (dis < 0).sum()
 
     def step():
         pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
@@ -183,16 +180,11 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-    if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)   # the only collective
+    D.reduce_stats(stats)        # the only collective
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
     total = B * world * a.steps
     value = total / elapsed
     if rank == 0:
@@ -218,8 +210,10 @@ def main():
                          "tree_kernel_ms": round(tm["tree_ms"], 4),
                          "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
                          "flop_model_per_solve": F_mod},
-            "closed_loop": {"J_mean": float(st_h[0] / max(st_h[4], 1)), "infeasible": int(st_h[2]),
-                            "iters_mean": float(st_h[3] / max(st_h[4], 1)), "collisions": int(st_h[5])},
+            "closed_loop": {"J_mean": float(st_h[D.STAT_J] / max(st_h[D.STAT_SOLVES], 1)),
+                            "infeasible": int(st_h[D.STAT_INFEAS]),
+                            "iters_mean": float(st_h[D.STAT_ITERS] / max(st_h[D.STAT_SOLVES], 1)),
+                            "collision_steps": int(st_h[D.STAT_COLL])},
         }
         if not a.no_cpu_baseline and world == 1:
             procs = max(1, min(8, len(os.sched_getaffinity(0))))

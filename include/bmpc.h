@@ -116,6 +116,7 @@ enum {
   BMPC_INFO_NCONES,     /* second-order cones                    */
   BMPC_INFO_LP,         /* LP rows (dims['l'])                   */
   BMPC_INFO_BATCH,
+  BMPC_INFO_WS_DOUBLES, /* per-ego HBM workspace slab (doubles)  */
   BMPC_INFO_COUNT
 };
 

@@ -78,6 +78,7 @@ int hs_info(void* p, int32_t* info) {
   info[BMPC_INFO_NCONES] = P.ncones;
   info[BMPC_INFO_LP] = P.nlp;
   info[BMPC_INFO_BATCH] = h->batch;
+  info[BMPC_INFO_WS_DOUBLES] = (int32_t)h->hp.lay.stride;
   return 0;
 }
 
