@@ -85,22 +85,24 @@ class BatchPlan:
         check(lib().bmpc_solve_device(self._h, *vp), "bmpc_solve_device")
 
     def get_warm_start(self):
-        """Checkpoint of the per-ego warm start (uLin, p, Jcons)."""
+        """Checkpoint of the per-ego warm start (uLin, p, Jcons, OldInput)."""
         B, d = self.batch, self.desc.d
         uLin = np.zeros((B, self.U + 1, d))
         p = np.zeros((B, self.bdim, self.desc.m))
         jc = np.zeros(B)
-        check(lib().bmpc_get_warm_start(self._h, _p(uLin), _p(p), _p(jc)), "bmpc_get_warm_start")
-        return dict(uLin=uLin, p=p, jcons=jc)
+        old = np.zeros((B, d))
+        check(lib().bmpc_get_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(old)), "bmpc_get_warm_start")
+        return dict(uLin=uLin, p=p, jcons=jc, old_input=old)
 
-    def set_warm_start(self, uLin, p, jcons, mask=None):
-        """Resume from a checkpoint (the next solve runs updatetree)."""
+    def set_warm_start(self, uLin, p=None, jcons=None, old_input=None, mask=None):
+        """Resume from a checkpoint (the next solve runs updatetree); None keeps a part."""
         B, d = self.batch, self.desc.d
         uLin = np.ascontiguousarray(np.asarray(uLin, np.float64).reshape(B, self.U + 1, d))
-        p = np.ascontiguousarray(np.asarray(p, np.float64).reshape(B, self.bdim, self.desc.m))
-        jc = np.ascontiguousarray(np.asarray(jcons, np.float64).reshape(B))
+        p = None if p is None else np.ascontiguousarray(np.asarray(p, np.float64).reshape(B, self.bdim, self.desc.m))
+        jc = None if jcons is None else np.ascontiguousarray(np.asarray(jcons, np.float64).reshape(B))
+        old = None if old_input is None else np.ascontiguousarray(np.asarray(old_input, np.float64).reshape(B, d))
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
-        check(lib().bmpc_set_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(m)), "bmpc_set_warm_start")
+        check(lib().bmpc_set_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(old), _p(m)), "bmpc_set_warm_start")
 
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d

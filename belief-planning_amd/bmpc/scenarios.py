@@ -73,3 +73,18 @@ def xref_rule(x, z, v0=20.0):
                     z[:, 2] + 1 * (z[:, 0] + 1.5 - x[:, 0]))
     xref = np.stack([np.zeros(B), Ydes, vdes, np.zeros(B)], axis=1)
     return xref, tgt
+
+
+def quadruped_desc(N=25, NB=2, vxm=0.2, vym=0.1, rm=0.5, dt=0.2, L1=0.5, W1=0.3, L2=1.0, W2=0.6,
+                   col_tol=0.2, s1=2.0):
+    """initquadBranchMPC(3,3,N,NB,...) + the main_quadruped.py:15-30 constants
+    (BranchMPCProx controller, 2 policies)."""
+    Fu = np.kron(np.eye(3), np.array([1, -1])).T
+    bu = np.array([vxm, 0.0, vym, vym, rm, rm])
+    return abi.make_desc(abi.CTRL_PROX, abi.MODEL_QUADRUPED, 3, 3, N, NB, 2, dt, np.eye(3),
+                         np.diag([1., 100., 1.]), np.zeros((0, 3)), [], Fu, bu, [0., 300.],
+                         [L1, W1, L2, W2, col_tol, s1], dR=[0.9, 5.0, 1.0])
+
+
+def quadruped_policy_rows(B, v0=0.2):
+    return [[(abi.POL_FORWARD, (v0,)), (abi.POL_STOP, ())] for _ in range(B)]

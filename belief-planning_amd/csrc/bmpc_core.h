@@ -99,6 +99,8 @@ struct Layout {
   // KKT
   size_t hx, hu, sd, P, Kg, Luu, kff, lvec, gk, colk, colnu;
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
+  // BranchMPCProx QP: u-rate couplings, linear cost, augmented Riccati P~, [Kx Kv], l~
+  size_t qo, qq, Pa, Ka, la;
   size_t stride;  // doubles per ego
 };
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "bmpc_plan.h"
+#include "bmpc_qp.h"
 #include "bmpc_solve.h"
 
 using namespace bmpc;
@@ -117,6 +118,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
     for (int i = lane; i < P.nbranch - 1; i += 64) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
   if (lane == 0) {
     if (J) J[e] = w[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_qp(
+    const Bundle* __restrict__ B, double* __restrict__ ws, const bmpc_policy* __restrict__ pol, double* upred,
+    double* xpred, double* bw, double* J, int32_t* status, int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  extern __shared__ double lds_dyn[];
+  DevExec ex{(int)threadIdx.x, lds_dyn};
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r = solve_ego_qp<DevExec, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += 64) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += 64) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += 64) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = r.pcost;
     if (status) status[e] = r.exit_flag;
     if (iters) iters[e] = r.iters;
   }
@@ -350,12 +378,13 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                        d_x, d_z, d_xref, B);
   HIPCHECK(hipGetLastError());
   if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[1], s));
+  const bool qp = P.desc.controller == BMPC_CTRL_PROX;
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
-    hipLaunchKernelGGL(k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol,
-                       d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+    hipLaunchKernelGGL(qp ? k_qp<Highway> : k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
+                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   else
-    hipLaunchKernelGGL(k_ipm<Quadruped>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol,
-                       d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+    hipLaunchKernelGGL(qp ? k_qp<Quadruped> : k_ipm<Quadruped>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
+                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   HIPCHECK(hipGetLastError());
   if (pl->timing) {
     HIPCHECK(hipEventRecord(pl->ev[2], s));
@@ -433,7 +462,7 @@ int bmpc_get_counters(bmpc_plan* pl, double* out) {
   return gather(pl, pl->hp.lay.prof, PROF_COUNT, out);
 }
 
-int bmpc_get_warm_start(bmpc_plan* pl, double* uLin, double* p, double* jcons) {
+int bmpc_get_warm_start(bmpc_plan* pl, double* uLin, double* p, double* jcons, double* old_input) {
   if (!pl) return fail(-22, "null argument");
   HIPCHECK(hipSetDevice(pl->ctx->device));
   const Plan& P = pl->hp.plan;
@@ -442,39 +471,40 @@ int bmpc_get_warm_start(bmpc_plan* pl, double* uLin, double* p, double* jcons) {
   if ((rc = gather(pl, L.uLin, (P.U + 1) * P.d, uLin))) return rc;
   if (P.bdim * P.m > 0 && (rc = gather(pl, L.pprev, P.bdim * P.m, p))) return rc;
   if ((rc = gather(pl, L.misc + MISC_JCONS, 1, jcons))) return rc;
+  if ((rc = gather(pl, L.misc + MISC_OLDU, P.d, old_input))) return rc;
   return 0;
 }
 
 int bmpc_set_warm_start(bmpc_plan* pl, const double* uLin, const double* p, const double* jcons,
-                        const uint8_t* mask) {
-  if (!pl || !uLin || !jcons) return fail(-22, "null argument");
+                        const double* old_input, const uint8_t* mask) {
+  if (!pl || !uLin) return fail(-22, "null argument");
   HIPCHECK(hipSetDevice(pl->ctx->device));
   const Plan& P = pl->hp.plan;
   const Layout& L = pl->hp.lay;
   const int B = pl->batch;
-  const int cu = (P.U + 1) * P.d, cp = P.bdim * P.m;
-  const size_t need = (size_t)B * (cu + cp + 2);
-  double* buf = nullptr;
   uint8_t* dmask = nullptr;
-  HIPCHECK(hipMalloc(&buf, need * sizeof(double)));
-  if (mask) HIPCHECK(hipMalloc(&dmask, B));
+  if (mask) {
+    HIPCHECK(hipMalloc(&dmask, B));
+    HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
+  }
   std::vector<double> ones(B, 1.0);
-  HIPCHECK(hipMemcpy(buf, uLin, sizeof(double) * B * cu, hipMemcpyHostToDevice));
-  if (cp && p) HIPCHECK(hipMemcpy(buf + (size_t)B * cu, p, sizeof(double) * B * cp, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(buf + (size_t)B * (cu + cp), jcons, sizeof(double) * B, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(buf + (size_t)B * (cu + cp + 1), ones.data(), sizeof(double) * B, hipMemcpyHostToDevice));
-  if (mask) HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.uLin, cu, buf, dmask, B);
-  if (cp && p)
-    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.pprev, cp,
-                       buf + (size_t)B * cu, dmask, B);
-  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.misc + MISC_JCONS, 1,
-                     buf + (size_t)B * (cu + cp), dmask, B);
-  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, L.misc + MISC_INIT, 1,
-                     buf + (size_t)B * (cu + cp + 1), dmask, B);
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipStreamSynchronize(pl->stream));
-  hipFree(buf);
+  struct Part { const double* src; size_t off; int cnt; };
+  const Part parts[] = {{uLin, L.uLin, (P.U + 1) * P.d},
+                        {p, L.pprev, P.bdim * P.m},
+                        {jcons, L.misc + MISC_JCONS, 1},
+                        {old_input, L.misc + MISC_OLDU, P.d},
+                        {ones.data(), L.misc + MISC_INIT, 1}};
+  for (const Part& pt : parts) {
+    if (!pt.src || pt.cnt <= 0) continue;
+    double* buf = nullptr;
+    HIPCHECK(hipMalloc(&buf, sizeof(double) * (size_t)B * pt.cnt));
+    HIPCHECK(hipMemcpy(buf, pt.src, sizeof(double) * (size_t)B * pt.cnt, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, pt.off, pt.cnt, buf,
+                       dmask, B);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(pl->stream));
+    hipFree(buf);
+  }
   if (dmask) hipFree(dmask);
   return 0;
 }

@@ -98,7 +98,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   memset(&P, 0, sizeof(P));
   P.desc = desc;
   const int n = desc.n, d = desc.d, N = desc.N, NB = desc.NB, m = desc.m;
-  if (desc.controller != BMPC_CTRL_CVAR) return "only the BranchMPC_CVaR controller is built in this version";
+  if (desc.controller != BMPC_CTRL_CVAR && desc.controller != BMPC_CTRL_PROX) return "unknown controller";
   if (desc.model == BMPC_MODEL_HIGHWAY) {
     if (n != 4 || d != 2) return "highway model needs n=4, d=2";
   } else if (desc.model == BMPC_MODEL_QUADRUPED) {
@@ -272,6 +272,25 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   hp.u_cone[0] = k;
   row += 2 + d;
   P.nrows = row;
+  if (desc.controller == BMPC_CTRL_PROX) {
+    // BranchMPCProx's OSQP vector z = [X | U | S] and rows [Fx-type | Fu | -S] (MPC_branch.py:185-370)
+    P.oS = T * n + U * d;
+    P.oRho = P.oSig = P.oMup = P.oMum = P.oS;   // no CVaR globals
+    P.oJ = P.oS + T * P.Nc;     // (no J; keeps "oS..oJ" = slack range for shared loops)
+    P.ncones = 0;
+    P.nv = P.oJ;
+    P.neq = T * n;
+    P.rFx = 0;
+    P.rFu = T * P.Nc;
+    P.rRisk = P.rFu + U * P.nFu;
+    P.rPos = P.rRisk;
+    P.nlp = P.rPos + T * P.Nc;
+    P.nrows = P.nlp;
+    P.ng = 0;
+    P.nsm = 0;
+    P.lds_M = P.lds_piv = P.lds_rhs = P.lds_red = 0;
+    P.nlds = 64;
+  }
 
   // ---- weights -----------------------------------------------------------------------------
   double Qm[BMPC_MAX_N * BMPC_MAX_N], Rm[BMPC_MAX_D * BMPC_MAX_D];
@@ -378,12 +397,22 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.P = take((size_t)T * n * n);
   L.Kg = take((size_t)U * d * n);
   L.Luu = take((size_t)U * d * d);
-  L.kff = take((size_t)nc * U * d);
+  L.kff = take((size_t)(nc > 0 ? nc : 1) * U * d);   // (PROX: one rhs)
   L.lvec = take((size_t)nc * T * n);
   L.gk = take((size_t)nc * nv);
   L.colk = take((size_t)nc * nv);
   L.colnu = take((size_t)nc * neq);
   L.prof = take(PROF_COUNT);
+  if (desc.controller == BMPC_CTRL_PROX) {   // QP-only arrays (augmented-state Riccati)
+    const int NS = n + d;
+    L.qo = take((size_t)U * d * d);
+    L.qq = take(nv);
+    L.Pa = take((size_t)T * NS * NS);
+    L.Ka = take((size_t)U * d * NS);
+    L.la = take((size_t)T * NS);
+  } else {
+    L.qo = L.qq = L.Pa = L.Ka = L.la = 0;
+  }
   L.stride = o;
   return "";
 }

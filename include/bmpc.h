@@ -14,6 +14,7 @@
  *   bmpc_reset         <- "self.BT is None" first-solve path (inittree) MPC_branch.py:2062-2064
  *   bmpc_solve         <- BranchMPC_CVaR.solve           MPC_branch.py:2043-2092
  *                         BranchMPCProx.solve             MPC_branch.py:384-423
+ *                         (BMPC_CTRL_PROX: OSQP QP, status 1 = solved / -2 = not)
  *                         (tree update, linearisation, assembly, ecos.solve / OSQP, unpack)
  *   bmpc_get_tree      <- BranchTree fields + BT2array    MPC_branch.py:65-78,2108-2122
  *   bmpc_model_eval    <- PredictiveModel.dyn_linearization / branch_eval / zpred_eval /
@@ -157,11 +158,13 @@ int bmpc_solve_device(bmpc_plan* plan, const double* d_x, const double* d_z,
 /* Checkpoint / resume of the per-ego warm start: the state the reference keeps
  * in the controller object between solves -- uLin [batch][U+1][d] (shifted by updatetree,
  * MPC_branch.py:1813-1823), the previous branch probabilities p [batch][bdim][m] (argmax
- * child, :1818) and the frozen Jcons [batch] (:1939).  set marks the egos as initialised
- * (the next solve runs updatetree, not inittree); mask NULL = all egos. */
-int bmpc_get_warm_start(bmpc_plan* plan, double* uLin, double* p, double* jcons);
+ * child, :1818), the frozen Jcons [batch] (CVaR, :1939) and OldInput [batch][d] (the rate
+ * cost of BranchMPCProx, :311,:421).  set marks the egos as initialised (the next solve runs
+ * updatetree, not inittree); NULL p / jcons / old_input keep the current values; mask NULL
+ * = all egos. */
+int bmpc_get_warm_start(bmpc_plan* plan, double* uLin, double* p, double* jcons, double* old_input);
 int bmpc_set_warm_start(bmpc_plan* plan, const double* uLin, const double* p,
-                        const double* jcons, const uint8_t* mask);
+                        const double* jcons, const double* old_input, const uint8_t* mask);
 
 /* Tree of the last solve (host copies; NULL skips):
  *   xbar,zbar [batch][T][n]  ubar [batch][U][d]  w [batch][nbranch]

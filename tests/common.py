@@ -35,6 +35,7 @@ def cone_problem(g, step):
 
 
 from bmpc.scenarios import (LANES, highway_desc, highway_desc_from_golden, highway_policy_rows,  # noqa: E402,F401
+                            quadruped_desc, quadruped_policy_rows,
                             seeded_batch, xref_rule)
 
 
@@ -68,3 +69,28 @@ def replay_batch(g, steps=None):
     jcons = np.full(T, xr0 @ np.asarray(g["Q"], float) @ xr0)      # frozen at the first solve (:1939)
     warm = ~np.isnan(np.asarray(g["traj_ws_uLin"][:T], float)).any(axis=(1, 2))
     return dict(x=x, z=z, xref=xref, rows=rows, uLin=uLin, p=pprev, jcons=jcons, warm=warm, T=T)
+
+
+def quadruped_desc_from_golden(g):
+    from bmpc.scenarios import quadruped_desc
+    d = quadruped_desc(N=int(g["N"]), NB=int(g["NB"]), vxm=float(g["vxm"]), vym=float(g["vym"]), rm=float(g["rm"]),
+                       dt=float(g["dt"]), L1=float(g["L1"]), W1=float(g["W1"]), L2=float(g["L2"]), W2=float(g["W2"]),
+                       col_tol=float(g["col_tol"]))
+    # the desc must carry exactly the reference's Init_MPC numbers
+    np.testing.assert_array_equal(np.array(d.Q[:9]).reshape(3, 3), g["Q"])
+    np.testing.assert_array_equal(np.array(d.R[:9]).reshape(3, 3), g["R"])
+    np.testing.assert_array_equal(np.array(d.dR[:3]), g["dR"])
+    np.testing.assert_array_equal(np.array(d.Fu[:18]).reshape(6, 3), g["Fu"])
+    np.testing.assert_array_equal(np.array(d.bu[:6]), g["bu"])
+    return d
+
+
+def quad_replay_batch(g, steps=None):
+    """Every recorded step of the quadruped loop as one ego, with the warm start
+    (uLin, p, OldInput) the reference BranchMPCProx carried into that solve."""
+    T = len(g["traj_x"]) if steps is None else min(steps, len(g["traj_x"]))
+    ws_u = np.asarray(g["traj_ws_uLin"][:T], float)
+    return dict(x=np.asarray(g["traj_x"][:T], float), z=np.asarray(g["traj_z"][:T], float),
+                xref=np.asarray(g["traj_xRef"][:T], float), uLin=np.nan_to_num(ws_u),
+                p=np.nan_to_num(np.asarray(g["traj_ws_p"][:T], float)),
+                old=np.asarray(g["traj_ws_old"][:T], float), warm=~np.isnan(ws_u).any(axis=(1, 2)), T=T)

@@ -107,25 +107,38 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
     if (upred) memcpy(upred + (size_t)e * P.U * P.d, ws + L.upred, sizeof(double) * P.U * P.d);
     if (xpred) memcpy(xpred + (size_t)e * P.T * P.n, ws + L.xpred, sizeof(double) * P.T * P.n);
     if (bw) memcpy(bw + (size_t)e * (P.nbranch - 1), ws + L.w + 1, sizeof(double) * (P.nbranch - 1));
-    if (J) J[e] = ws[L.sol + P.oJ];
+    if (J) J[e] = P.desc.controller == BMPC_CTRL_PROX ? r.pcost : ws[L.sol + P.oJ];
     if (status) status[e] = r.exit_flag;
     if (iters) iters[e] = r.iters;
   }
   return 0;
 }
 
-int hs_set_warm_start(void* p, const double* uLin, const double* pprev, const double* jcons) {
+int hs_set_warm_start(void* p, const double* uLin, const double* pprev, const double* jcons,
+                      const double* oldu) {
   HS* h = (HS*)p;
   const Plan& P = h->hp.plan;
   const Layout& L = h->hp.lay;
   for (int e = 0; e < h->batch; ++e) {
     double* ws = h->ws.data() + L.stride * e;
     memcpy(ws + L.uLin, uLin + (size_t)e * (P.U + 1) * P.d, sizeof(double) * (P.U + 1) * P.d);
-    memcpy(ws + L.pprev, pprev + (size_t)e * P.bdim * P.m, sizeof(double) * P.bdim * P.m);
-    ws[L.misc + MISC_JCONS] = jcons[e];
+    if (pprev) memcpy(ws + L.pprev, pprev + (size_t)e * P.bdim * P.m, sizeof(double) * P.bdim * P.m);
+    if (jcons) ws[L.misc + MISC_JCONS] = jcons[e];
+    if (oldu) memcpy(ws + L.misc + MISC_OLDU, oldu + (size_t)e * P.d, sizeof(double) * P.d);
     ws[L.misc + MISC_INIT] = 1.0;
   }
   return 0;
+}
+
+// debugging aids: raw workspace of ego e and the Layout offsets (sizeof(Layout)/8 size_t)
+double* hs_ws_ptr(void* p, int e) {
+  HS* h = (HS*)p;
+  return h->ws.data() + h->hp.lay.stride * e;
+}
+int hs_layout(void* p, size_t* out) {
+  HS* h = (HS*)p;
+  memcpy(out, &h->hp.lay, sizeof(Layout));
+  return (int)(sizeof(Layout) / sizeof(size_t));
 }
 
 int hs_reset(void* p, const uint8_t* mask) {

@@ -85,16 +85,34 @@ class HostSim:
         lib().hs_solve(self.h, _p(x), _p(z), _p(xref), _p(up), _p(xp), _p(bw), _p(J), _p(st), _p(it))
         return dict(upred=up, xpred=xp, branch_w=bw, J=J, status=st, iters=it)
 
-    def set_warm_start(self, uLin, pprev, jcons):
+    def set_warm_start(self, uLin, pprev, jcons=None, oldu=None):
         B = self.batch
         uLin = np.ascontiguousarray(np.asarray(uLin, float).reshape(B, self.U + 1, self.desc.d))
         pprev = np.ascontiguousarray(np.asarray(pprev, float).reshape(B, self.bdim, self.desc.m))
-        jcons = np.ascontiguousarray(np.asarray(jcons, float).reshape(B))
-        lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons))
+        jcons = None if jcons is None else np.ascontiguousarray(np.asarray(jcons, float).reshape(B))
+        oldu = None if oldu is None else np.ascontiguousarray(np.asarray(oldu, float).reshape(B, self.desc.d))
+        lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons), _p(oldu))
 
     def reset_mask(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         lib().hs_reset(self.h, _p(m))
+
+    def layout(self):
+        """Layout offsets by field name (parsed from csrc/bmpc_core.h, declaration order)."""
+        import re
+        src = open(os.path.join(PKG, "csrc", "bmpc_core.h")).read()
+        body = src[src.index("struct Layout {"):src.index("};", src.index("struct Layout {"))]
+        names = [n for line in body.splitlines() if line.strip().startswith("size_t")
+                 for n in re.findall(r"(\w+)\s*[,;]", line.split("size_t", 1)[1])]
+        out = np.zeros(256, np.uint64)
+        cnt = lib().hs_layout(self.h, _p(out))
+        assert cnt == len(names), (cnt, names)
+        return dict(zip(names, (int(v) for v in out[:cnt])))
+
+    def workspace(self, e=0):
+        lib().hs_ws_ptr.restype = C.POINTER(C.c_double)
+        ptr = lib().hs_ws_ptr(self.h, e)
+        return np.ctypeslib.as_array(ptr, shape=(self.layout()["stride"],))
 
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d

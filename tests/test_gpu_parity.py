@@ -120,3 +120,44 @@ def test_full_batch_certified(gpu):
         c.solve(x[e], z[e], xref[e])
         assert abs(r["J"][e] - c.last_info["x"][-1]) <= 1e-6 * max(1, abs(r["J"][e]))
         np.testing.assert_allclose(r["upred"][e, 0], c.uPred[0], atol=1e-4)
+
+
+def test_quadruped_prox_replay_gpu(gpu):
+    """BranchMPCProx (BASELINE config 4): every recorded step of the reference quadruped loop
+    as one ego of one batched launch, with its warm start (uLin, p, OldInput); status_val 1
+    and uPred[0] to 1e-6 (the oracle QP optimum is exact to ~1e-10)."""
+    from common import quad_replay_batch, quadruped_desc_from_golden, quadruped_policy_rows
+    g = golden("quadruped_n25_nb2")
+    rb = quad_replay_batch(g)
+    pl = gpu.BatchPlan(quadruped_desc_from_golden(g), rb["T"])
+    pl.set_policies(quadruped_policy_rows(rb["T"]))
+    pl.set_warm_start(rb["uLin"], rb["p"], None, rb["old"], mask=rb["warm"])
+    r = pl.solve(rb["x"], rb["z"], rb["xref"])
+    np.testing.assert_array_equal(r["status"], np.ones(rb["T"]))
+    np.testing.assert_allclose(r["upred"][:, 0], g["traj_u"][:rb["T"]], atol=1e-6)
+    sol = pl.tree()["sol"]
+    for t in (int(k) for k in g["keep"]):
+        ref = g[f"s{t}_sol"]
+        np.testing.assert_allclose(sol[t], ref, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=f"step {t}")
+
+
+def test_quadruped_model_eval_matches_oracle(gpu):
+    from oracle.model import QuadrupedModel, quadruped_policies
+    from common import quadruped_desc, quadruped_policy_rows
+    rng = np.random.default_rng(5)
+    B = 128
+    desc = quadruped_desc()
+    x = np.stack([rng.uniform(-2, 6, B), rng.uniform(-4, 4, B), rng.uniform(-np.pi, np.pi, B)], 1)
+    u = np.stack([rng.uniform(0, .2, B), rng.uniform(-.1, .1, B), rng.uniform(-.5, .5, B)], 1)
+    z = x + np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-1, 1, B)], 1)
+    out = gpu.model_eval(desc, quadruped_policy_rows(B), x, u, z)
+    mdl = QuadrupedModel(25, 0.2, quadruped_policies(0.2))
+    for b in range(0, B, 7):
+        A, Bm, C, xp = mdl.dyn_linearization(x[b], u[b])
+        p, dp = mdl.branch_eval(x[b], z[b])
+        h0, dh = mdl.col_eval(x[b], z[b])
+        zp = mdl.zpred_eval(z[b])
+        for got, ref in ((out["A"][b], A), (out["B"][b], Bm), (out["C"][b], C), (out["xp"][b], xp),
+                         (out["p"][b], p), (out["dp"][b], dp), (out["zpred"][b], zp),
+                         (out["h0"][b], h0), (out["dh"][b], dh)):
+            np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)

@@ -205,7 +205,7 @@ def gen_quadruped(name, steps, keep, out):
     # the build's own quadruped loop (quadruped_env.py:67-130 crashes at :120; same rules)
     x_des = np.array([5., -3., 0.])
     ego = np.array([0, 1.8, 0.]); obs = np.array([2.5, 2.5, -np.pi / 2])
-    traj = {k: [] for k in ("x", "z", "xRef", "u", "status")}
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "status", "ws_uLin", "ws_p", "ws_old")}
     for t in range(steps):
         dx = x_des[0:2] - ego[0:2]
         dx = dx / np.linalg.norm(dx) * min(np.linalg.norm(dx), 5.0)
@@ -218,6 +218,11 @@ def gen_quadruped(name, steps, keep, out):
         else:
             psiRef = ego[2]
         xr = ego.copy(); xr[0:2] += dx; xr[2] = psiRef
+        # warm start carried into this solve (updatetree inputs) and the rate-cost OldInput
+        traj["ws_uLin"].append(None if mpc.uLin is None else np.array(mpc.uLin, float).copy())
+        traj["ws_p"].append(None if mpc.BT is None else
+                            np.array([np.ravel(b.p) for b in mpc.ndx if b.depth < NB], float))
+        traj["ws_old"].append(np.array(mpc.OldInput, float).reshape(-1).copy())
         mpc.solve(ego.copy(), obs.copy(), xr)
         prob, sol, info, kw = CURRENT["captured"]
         assert kw == {"verbose": False, "polish": True}, kw
@@ -244,6 +249,9 @@ def gen_quadruped(name, steps, keep, out):
         obs = obs + np.array([uo[0] * np.cos(obs[2]) - uo[1] * np.sin(obs[2]),
                               uo[1] * np.cos(obs[2]) + uo[0] * np.sin(obs[2]), uo[2]]) * dt
         print(f"[{name}] t={t} status={info['status_val']} u0={u}", flush=True)
+    for k in ("ws_uLin", "ws_p"):
+        shape = next(v.shape for v in traj[k] if v is not None)
+        traj[k] = [np.full(shape, np.nan) if v is None else v for v in traj[k]]
     for k, v in traj.items():
         d_out["traj_" + k] = np.array(v)
     d_out["keep"] = np.array(sorted(keep))
@@ -264,7 +272,7 @@ def main():
         "highway_n8_nb2": lambda: gen_highway("highway_n8_nb2", 8, 2, 5 if a.quick else 40, {0, 1, 2, 30}, out),
         "highway_n10_nb1": lambda: gen_highway("highway_n10_nb1", 10, 1, 5 if a.quick else 20, {0, 1}, out),
         "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 2, {0, 1}, out),
-        "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 10, {0, 1, 2}, out),
+        "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
     }
     for k, f in jobs.items():
         if a.only and k not in a.only.split(","):
