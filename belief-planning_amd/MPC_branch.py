@@ -246,9 +246,24 @@ class _NotBuilt:
                                   "(see DESIGN.md, scope)")
 
 
-class BranchMPCProx(_NotBuilt):
-    """Proximal branch QP (MPC_branch.py:82-488) -- next row of SURVEY §8."""
-    _what = "BranchMPCProx (quadruped QP)"
+class BranchMPCProx(BranchMPC_CVaR):
+    """Proximal branch QP (MPC_branch.py:82-488) on MI355X: the OSQP problem of
+    buildCost/buildEqConstr/buildIneqConstr solved by the device QP interior point.
+    ``feasible`` follows osqp_solve_qp: only status_val == 1 (:482); otherwise the previous
+    prediction is kept, and OldInput = uPred[0] either way (:421)."""
+
+    controller_kind = abi.CTRL_PROX
+
+    def __init__(self, mpcParameters, predictiveModel, batch=1, device=0):
+        super().__init__(mpcParameters, predictiveModel, ralpha=0.0, batch=batch, device=device)
+
+    def solve(self, x, z, xRef=None):
+        """One controller step (MPC_branch.py:384-423)."""
+        super().solve(x, z, xRef)
+
+    def _unpack(self, r, e):
+        super()._unpack(r, e)
+        self.feasible = 1 if self.status == 1 else 0
 
 
 class BranchMPC(_NotBuilt):

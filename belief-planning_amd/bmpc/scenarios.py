@@ -88,3 +88,33 @@ def quadruped_desc(N=25, NB=2, vxm=0.2, vym=0.1, rm=0.5, dt=0.2, L1=0.5, W1=0.3,
 
 def quadruped_policy_rows(B, v0=0.2):
     return [[(abi.POL_FORWARD, (v0,)), (abi.POL_STOP, ())] for _ in range(B)]
+
+
+def seeded_quadruped_batch(B, seed=1):
+    """Synthetic quadruped egos (BASELINE config 4): ego in a 6 m x 6 m yard heading anywhere,
+    obstacle 1-4 m away walking at any heading; goal x_des = (5, -3, 0) as in the recorded
+    loop.  Row 0 is main_quadruped's state (ego (0, 1.8, 0), obstacle (2.5, 2.5, -pi/2))."""
+    rng = np.random.default_rng(seed)
+    x = np.stack([rng.uniform(-1, 1, B), rng.uniform(0, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+    r, a = rng.uniform(1, 4, B), rng.uniform(-np.pi, np.pi, B)
+    z = np.stack([x[:, 0] + r * np.cos(a), x[:, 1] + r * np.sin(a), rng.uniform(-np.pi, np.pi, B)], 1)
+    x[0] = [0, 1.8, 0]
+    z[0] = [2.5, 2.5, -np.pi / 2]
+    return x, z, quadruped_xref(x)
+
+
+def quadruped_xref(x, x_des=(5.0, -3.0, 0.0)):
+    """Reference of the recorded quadruped loop (tools/gen_golden.py, after quadruped_env.py):
+    a point at most 5 m towards x_des, heading along the way."""
+    x = np.atleast_2d(x)
+    xd = np.asarray(x_des, float)
+    dx = xd[None, 0:2] - x[:, 0:2]
+    nrm = np.linalg.norm(dx, axis=1)
+    dx = dx / np.maximum(nrm, 1e-300)[:, None] * np.minimum(nrm, 5.0)[:, None]
+    psi = np.arctan2(dx[:, 1], dx[:, 0])
+    psi = np.where(np.linalg.norm(dx, axis=1) > 0.1, psi, x[:, 2])
+    psi = psi - 2 * np.pi * np.round((psi - xd[2]) / (2 * np.pi))
+    xr = x.copy()
+    xr[:, 0:2] += dx
+    xr[:, 2] = psi
+    return xr

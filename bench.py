@@ -95,18 +95,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="egos per GPU")
-    ap.add_argument("--N", type=int, default=20)
-    ap.add_argument("--NB", type=int, default=1)
+    ap.add_argument("--workload", choices=("highway", "quadruped"), default="highway",
+                    help="highway = BASELINE metric config; quadruped = BASELINE config 4 (BranchMPCProx)")
+    ap.add_argument("--batch", type=int, default=None, help="egos per GPU (highway 4096, quadruped 1024)")
+    ap.add_argument("--N", type=int, default=None)
+    ap.add_argument("--NB", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=24)
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
     a = ap.parse_args()
+    quad = a.workload == "quadruped"
+    a.batch = a.batch or (1024 if quad else 4096)
+    a.N = a.N or (25 if quad else 20)
+    a.NB = a.NB or (2 if quad else 1)
 
     import torch
     import torch.distributed as dist
     from bmpc import plan
-    from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch
+    from bmpc.scenarios import (highway_desc, highway_policy_rows, quadruped_desc, quadruped_policy_rows,
+                                seeded_batch, seeded_quadruped_batch)
 
     from bmpc import distributed as D
     rank, local, world = D.world()
@@ -116,14 +123,20 @@ def main():
     B = a.batch
     # one global seeded population of B*world egos; rank r owns a contiguous shard
     lo, hi = D.shard(B * world, rank, world)
-    x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(B * world, seed=0))
-    desc = highway_desc(N=a.N, NB=a.NB)
-    pl = plan.BatchPlan(desc, B, device=local)
-    pl.set_policies(highway_policy_rows(tgt))
+    if quad:
+        x, z, xref = (v[lo:hi] for v in seeded_quadruped_batch(B * world, seed=1))
+        desc = quadruped_desc(N=a.N, NB=a.NB)
+        pl = plan.BatchPlan(desc, B, device=local)
+        pl.set_policies(quadruped_policy_rows(B))
+    else:
+        x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(B * world, seed=0))
+        desc = highway_desc(N=a.N, NB=a.NB)
+        pl = plan.BatchPlan(desc, B, device=local)
+        pl.set_policies(highway_policy_rows(tgt))
     tx = torch.tensor(x, device=dev, dtype=torch.float64)
     tz = torch.tensor(z, device=dev, dtype=torch.float64)
     tr = torch.tensor(xref, device=dev, dtype=torch.float64)
-    up = torch.zeros((B, pl.U, 2), device=dev, dtype=torch.float64)
+    up = torch.zeros((B, pl.U, desc.d), device=dev, dtype=torch.float64)
     Jv = torch.zeros(B, device=dev, dtype=torch.float64)
     st = torch.zeros(B, device=dev, dtype=torch.int32)
     it = torch.zeros(B, device=dev, dtype=torch.int32)
@@ -156,10 +169,36 @@ def main():
         stats[D.STAT_SOLVES] += B
         stats[D.STAT_COLL] += (dis < 0).sum()
 
+    qdt, qv0 = 0.2, 0.2
+    xdes = torch.tensor([5.0, -3.0, 0.0], device=dev, dtype=torch.float64)
+
+    def quad_env_step():
+        """robot.step of ego (uPred[0]) and obstacle (forward policy), body-frame kinematics
+        (quadruped_env.py:34-37), and the reference point towards x_des, on device."""
+        u0 = up[:, 0, :]
+        c, s_ = torch.cos(tx[:, 2]), torch.sin(tx[:, 2])
+        tx.copy_(tx + qdt * torch.stack([u0[:, 0] * c - u0[:, 1] * s_, u0[:, 1] * c + u0[:, 0] * s_, u0[:, 2]], 1))
+        tz.copy_(tz + qdt * torch.stack([qv0 * torch.cos(tz[:, 2]), qv0 * torch.sin(tz[:, 2]),
+                                          torch.zeros_like(tz[:, 2])], 1))
+        dxy = xdes[None, 0:2] - tx[:, 0:2]
+        nrm = torch.linalg.norm(dxy, dim=1)
+        dxy = dxy / nrm.clamp_min(1e-300)[:, None] * nrm.clamp_max(5.0)[:, None]
+        psi = torch.where(torch.linalg.norm(dxy, dim=1) > 0.1, torch.atan2(dxy[:, 1], dxy[:, 0]), tx[:, 2])
+        psi = psi - 2 * math.pi * torch.round((psi - xdes[2]) / (2 * math.pi))
+        tr[:, 0:2] = tx[:, 0:2] + dxy
+        tr[:, 2] = psi
+        dis = torch.linalg.norm(tx[:, 0:2] - tz[:, 0:2], dim=1) - 0.75
+        stats[D.STAT_J] += Jv.sum()
+        stats[D.STAT_J2] += (Jv * Jv).sum()
+        stats[D.STAT_INFEAS] += (st != 1).sum()
+        stats[D.STAT_ITERS] += it.sum()
+        stats[D.STAT_SOLVES] += B
+        stats[D.STAT_COLL] += (dis < 0).sum()
+
     def step():
         pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
                         Jv.data_ptr(), st.data_ptr(), it.data_ptr(), stream.cuda_stream)
-        env_step()
+        quad_env_step() if quad else env_step()
 
     for _ in range(a.warmup):
         step()
@@ -190,23 +229,31 @@ def main():
     if rank == 0:
         st_h = stats.cpu().numpy()
         T, U, bdim, nbr = pl.T, pl.U, pl.bdim, pl.nbranch
-        cone_dims = [2 + a.N * 6] * (bdim * 3) + [4]
-        F_it = flops_per_iter(T, 4, 2, 5, 4, cone_dims)
-        F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
+        if quad:   # same per-node formula, n = d = 3, Nc = 1, nFu = 6, no cones, m = 2
+            F_it = flops_per_iter(T, 3, 3, 1, 6, [])
+            F_mod = flops_model(U, nbr - 1, bdim, 2, a.N, 3)
+        else:
+            cone_dims = [2 + a.N * 6] * (bdim * 3) + [4]
+            F_it = flops_per_iter(T, 4, 2, 5, 4, cone_dims)
+            F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
         achieved = B * iters_mean * F_it / (tm["ipm_ms"] * 1e-3) / 1e12 if tm["ipm_ms"] > 0 else 0.0
-        traffic = load_traffic(a.traffic)
+        traffic = None if quad else load_traffic(a.traffic)
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
+            "metric": METRIC if not quad else "branch-MPC solves/sec (whole node), quadruped BranchMPCProx "
+                                              "N=25 NB=2 m=2 (4 leaves), batch 1024 egos",
+            "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)",
-            "config": {"workload": f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 "
-                                   f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
+            "config": {"workload": (f"quadruped BranchMPCProx closed loop, N={a.N}, NB={a.NB}, m=2 " if quad else
+                                    f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
+                                   + f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"ego-sharded dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
                          "traffic": traffic,
-                         "kernel": "k_ipm (structured HSDE IPM)", "kernel_ms": round(tm["ipm_ms"], 4),
+                         "kernel": "k_qp (structured Mehrotra QP IPM)" if quad else "k_ipm (structured HSDE IPM)",
+                         "kernel_ms": round(tm["ipm_ms"], 4),
                          "tree_kernel_ms": round(tm["tree_ms"], 4),
                          "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
                          "flop_model_per_solve": F_mod},
@@ -215,7 +262,7 @@ def main():
                             "iters_mean": float(st_h[D.STAT_ITERS] / max(st_h[D.STAT_SOLVES], 1)),
                             "collision_steps": int(st_h[D.STAT_COLL])},
         }
-        if not a.no_cpu_baseline and world == 1:
+        if not a.no_cpu_baseline and world == 1 and not quad:
             procs = max(1, min(8, len(os.sched_getaffinity(0))))
             cb = cpu_baseline(a.N, a.NB, a.cpu_sample, procs)
             out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
