@@ -266,9 +266,12 @@ class BranchMPCProx(BranchMPC_CVaR):
         self.feasible = 1 if self.status == 1 else 0
 
 
-class BranchMPC(_NotBuilt):
-    """Branch QP (MPC_branch.py:881-1274)."""
-    _what = "BranchMPC"
+class BranchMPC(BranchMPCProx):
+    """Branch QP -- the active (second) definition, MPC_branch.py:881-1274 -- on MI355X.
+    Same tree, constraints, OSQP feasibility rule and OldInput update as BranchMPCProx; the
+    cost is buildCost :1063-1110 (dQ = 0.5 Q, no rate couplings)."""
+
+    controller_kind = abi.CTRL_QP
 
 
 class robustMPC(_NotBuilt):

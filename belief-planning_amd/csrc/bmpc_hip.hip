@@ -378,7 +378,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                        d_x, d_z, d_xref, B);
   HIPCHECK(hipGetLastError());
   if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[1], s));
-  const bool qp = P.desc.controller == BMPC_CTRL_PROX;
+  const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(qp ? k_qp<Highway> : k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
                        pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);

@@ -98,7 +98,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   memset(&P, 0, sizeof(P));
   P.desc = desc;
   const int n = desc.n, d = desc.d, N = desc.N, NB = desc.NB, m = desc.m;
-  if (desc.controller != BMPC_CTRL_CVAR && desc.controller != BMPC_CTRL_PROX) return "unknown controller";
+  if (desc.controller != BMPC_CTRL_CVAR && desc.controller != BMPC_CTRL_PROX && desc.controller != BMPC_CTRL_QP)
+    return "unknown controller";
   if (desc.model == BMPC_MODEL_HIGHWAY) {
     if (n != 4 || d != 2) return "highway model needs n=4, d=2";
   } else if (desc.model == BMPC_MODEL_QUADRUPED) {
@@ -272,8 +273,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   hp.u_cone[0] = k;
   row += 2 + d;
   P.nrows = row;
-  if (desc.controller == BMPC_CTRL_PROX) {
-    // BranchMPCProx's OSQP vector z = [X | U | S] and rows [Fx-type | Fu | -S] (MPC_branch.py:185-370)
+  if (desc.controller != BMPC_CTRL_CVAR) {
+    // BranchMPCProx's / BranchMPC's OSQP vector z = [X | U | S] and rows [Fx-type | Fu | -S] (MPC_branch.py:185-370)
     P.oS = T * n + U * d;
     P.oRho = P.oSig = P.oMup = P.oMum = P.oS;   // no CVaR globals
     P.oJ = P.oS + T * P.Nc;     // (no J; keeps "oS..oJ" = slack range for shared loops)
@@ -403,7 +404,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.colk = take((size_t)nc * nv);
   L.colnu = take((size_t)nc * neq);
   L.prof = take(PROF_COUNT);
-  if (desc.controller == BMPC_CTRL_PROX) {   // QP-only arrays (augmented-state Riccati)
+  if (desc.controller != BMPC_CTRL_CVAR) {   // QP-only arrays (augmented-state Riccati)
     const int NS = n + d;
     L.qo = take((size_t)U * d * d);
     L.qq = take(nv);

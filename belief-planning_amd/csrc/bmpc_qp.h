@@ -47,21 +47,26 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     xqf[c] = b;
   }
   double* q = ws + L.qq;
+  // BranchMPCProx: dQ = 3Q (:270); BranchMPC: dQ = 0.5Q, leaf's last node tracks xRef with Qf
+  // and the leaf terminal node has no linear term (:1068-1099)
+  const bool prox = P.desc.controller == BMPC_CTRL_PROX;
+  const double dq = prox ? 3.0 : 0.5;
   // state nodes: Hx (doubled) and qx
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int b = t.x_branch[k];
     const double wb = w[b];
     const bool term = t.x_u[k] < 0;
+    const bool leaf_last = !term && t.br_child0[b] < 0 && k == t.br_ndx[b] + t.br_len[b] - 1;
     double* H = ws + L.hx + k * NX * NX;
-    for (int i = 0; i < NX * NX; ++i) H[i] = 2.0 * wb * (term ? Qf[i] : 4.0 * Q[i]);   // (dQ + Q) w, dQ = 3Q
+    for (int i = 0; i < NX * NX; ++i) H[i] = 2.0 * wb * (term ? Qf[i] : (dq + 1.0) * Q[i]);   // (dQ + Q) w
     for (int c = 0; c < NX; ++c) {
       double v;
       if (term) {
-        v = -2.0 * wb * xqf[c];
+        v = prox ? -2.0 * wb * xqf[c] : 0.0;
       } else {
         double xd = 0.0;
-        for (int r = 0; r < NX; ++r) xd += xbar[k * NX + r] * 3.0 * Q[r * NX + c];
-        v = -2.0 * wb * (xq[c] + xd);
+        for (int r = 0; r < NX; ++r) xd += xbar[k * NX + r] * dq * Q[r * NX + c];
+        v = -2.0 * wb * (((!prox && leaf_last) ? xqf[c] : xq[c]) + xd);
       }
       q[P.oX + k * NX + c] = v;
     }
@@ -78,7 +83,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     double D[NU][NU];
     for (int r = 0; r < NU; ++r)
       for (int c = 0; c < NU; ++c) D[r][c] = 0.0;
-    if (leaf && j == len - 1) {
+    if ((leaf && j == len - 1) || !prox) {   // assigned w R (BranchMPC: every block, :1077-1090)
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) D[r][c] = wb * R[r * NU + c];
     } else {
@@ -88,7 +93,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
         if (j >= 1 || b != 0) D[r][r] += wb * dR[r];
       }
     }
-    if (u == 0)   // Hu[0:d,0:d] += dR (row broadcast), upper triangle read by OSQP
+    if (u == 0 && prox)   // Hu[0:d,0:d] += dR (row broadcast), upper triangle read by OSQP
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) D[r][c] += dR[r > c ? r : c];
     double* Hu = ws + L.hu + u * NU * NU;
@@ -97,7 +102,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     for (int r = 0; r < NU; ++r)
       for (int c = 0; c < NU; ++c) {
         Hu[r * NU + c] = 2.0 * D[r][c];
-        O[r * NU + c] = (pu >= 0 && r == c) ? -2.0 * wb * dR[r] : 0.0;
+        O[r * NU + c] = (prox && pu >= 0 && r == c) ? -2.0 * wb * dR[r] : 0.0;
       }
     double od = 0.0;
     if (u == 0)

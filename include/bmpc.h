@@ -14,6 +14,7 @@
  *   bmpc_reset         <- "self.BT is None" first-solve path (inittree) MPC_branch.py:2062-2064
  *   bmpc_solve         <- BranchMPC_CVaR.solve           MPC_branch.py:2043-2092
  *                         BranchMPCProx.solve             MPC_branch.py:384-423
+ *                         BranchMPC.solve                 MPC_branch.py:1171-1210
  *                         (BMPC_CTRL_PROX: OSQP QP, status 1 = solved / -2 = not)
  *                         (tree update, linearisation, assembly, ecos.solve / OSQP, unpack)
  *   bmpc_get_tree      <- BranchTree fields + BT2array    MPC_branch.py:65-78,2108-2122
@@ -49,7 +50,8 @@ extern "C" {
 /* controller kinds */
 enum {
   BMPC_CTRL_CVAR = 0, /* BranchMPC_CVaR  (ECOS SOCP)   MPC_branch.py:1598 */
-  BMPC_CTRL_PROX = 1  /* BranchMPCProx   (OSQP QP)     MPC_branch.py:82   */
+  BMPC_CTRL_PROX = 1, /* BranchMPCProx   (OSQP QP)     MPC_branch.py:82   */
+  BMPC_CTRL_QP = 2    /* BranchMPC, active definition (OSQP QP) MPC_branch.py:881 */
 };
 
 /* predictive models */

@@ -650,3 +650,47 @@ class ProxController:
 
     def BT2array(self):
         return self.tree.bt2array()
+
+
+class BranchQPController(ProxController):
+    """Oracle restatement of ``BranchMPC`` -- the active (second) definition,
+    MPC_branch.py:881-1274.  Same tree, constraints and OSQP call as ``BranchMPCProx``; the
+    cost differs (``buildCost`` :1063-1110): dQ = 0.5 Q, Hu blocks are *assigned* w R (no
+    rate couplings, no dR broadcast), the leaf's last node tracks xRef with Qf and the leaf
+    terminal node has no linear term; qu[0:d] = -2 OldInput.dR stays (:1102)."""
+
+    def build_cost(self):
+        t, n, d = self.topo, self.n, self.d
+        tr = self.tree
+        dQ = 0.5 * self.Q
+        Hx = [np.zeros((n, n)) for _ in range(t.T)]
+        Hu = np.zeros((t.U * d, t.U * d))
+        qx = np.zeros(t.T * n)
+        xq = self.xRef @ self.Q
+
+        def ublk(a):
+            return (slice(a * d, (a + 1) * d), slice(a * d, (a + 1) * d))
+
+        for b in range(t.nbranch):
+            w = tr.w[b]
+            ndx, ndu, l = t.ndx[b], t.ndu[b], t.length[b]
+            for i in range(l - 1):
+                Hx[ndx + i] = (dQ + self.Q) * w
+                qx[(ndx + i) * n:(ndx + i + 1) * n] = -2 * w * (xq + tr.xtraj[b][i] @ dQ)
+                Hu[ublk(ndu + i)] = w * self.R
+            Hu[ublk(ndu + l - 1)] = w * self.R
+            Hx[ndx + l - 1] = (dQ + self.Q) * w
+            if not t.is_leaf(b):
+                childJ = np.zeros(self.m)                    # BranchTree.J is always 0 (:76)
+                qx[(ndx + l - 1) * n:(ndx + l) * n] = w * (-2 * xq - 2 * tr.xtraj[b][l - 1] @ dQ
+                                                          + childJ @ tr.dp[b])
+            else:
+                Hx[ndx + l] = self.Qf * w
+                qx[(ndx + l - 1) * n:(ndx + l) * n] = -2 * w * (self.xRef @ self.Qf + tr.xtraj[b][l - 1] @ dQ)
+        qu = np.zeros(t.U * d)
+        qu[0:d] = -2 * (self.OldInput @ self.dR)           # scalar broadcast (:1102)
+        nS = t.T * self.Nc
+        H = sp.block_diag([sp.block_diag(Hx), sp.csc_matrix(Hu),
+                           self.Qslack[0] * sp.eye(nS)], format='csc')
+        qv = np.concatenate([qx, qu, self.Qslack[1] * self.slackweight])
+        return 2.0 * H, qv

@@ -107,7 +107,7 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
     if (upred) memcpy(upred + (size_t)e * P.U * P.d, ws + L.upred, sizeof(double) * P.U * P.d);
     if (xpred) memcpy(xpred + (size_t)e * P.T * P.n, ws + L.xpred, sizeof(double) * P.T * P.n);
     if (bw) memcpy(bw + (size_t)e * (P.nbranch - 1), ws + L.w + 1, sizeof(double) * (P.nbranch - 1));
-    if (J) J[e] = P.desc.controller == BMPC_CTRL_PROX ? r.pcost : ws[L.sol + P.oJ];
+    if (J) J[e] = P.desc.controller != BMPC_CTRL_CVAR ? r.pcost : ws[L.sol + P.oJ];
     if (status) status[e] = r.exit_flag;
     if (iters) iters[e] = r.iters;
   }

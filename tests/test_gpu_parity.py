@@ -161,3 +161,20 @@ def test_quadruped_model_eval_matches_oracle(gpu):
                          (out["p"][b], p), (out["dp"][b], dp), (out["zpred"][b], zp),
                          (out["h0"][b], h0), (out["dh"][b], dh)):
             np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_branch_mpc_qp_replay_gpu(gpu):
+    """BranchMPC (MPC_branch.py:881) highway scene, every recorded step in one launch."""
+    from bmpc import abi
+    g = golden("highway_qp_n8_nb2")
+    T = len(g["traj_x"])
+    desc = highway_desc_from_golden(g)
+    desc.controller = abi.CTRL_QP
+    pl = gpu.BatchPlan(desc, T)
+    pl.set_policies(highway_policy_rows(g["traj_lc_target"], float(g["Kpsi"])))
+    ws_u = np.asarray(g["traj_ws_uLin"], float)
+    warm = ~np.isnan(ws_u).any(axis=(1, 2))
+    pl.set_warm_start(np.nan_to_num(ws_u), np.nan_to_num(g["traj_ws_p"]), None, g["traj_ws_old"], mask=warm)
+    r = pl.solve(g["traj_x"], g["traj_z"], g["traj_xRef"])
+    np.testing.assert_array_equal(r["status"], g["traj_status"])
+    np.testing.assert_allclose(r["upred"][:, 0], g["traj_u"], atol=1e-6)

@@ -81,3 +81,62 @@ def test_oracle_ipm_certifies_reference_problems(name):
         assert r["eq"] < 1e-9 and r["ineq"] < 1e-7 and r["dual"] < 1e-5 and r["cone"] > -1e-6
         assert abs(r["pcost"] - r["dcost"]) <= 1e-6 * max(1.0, abs(r["pcost"]))
         assert abs(x[-1] - g[f"s{t}_sol"][-1]) <= 1e-9 * max(1, abs(x[-1]))
+
+
+def _inject_ws(c, g, t):
+    """The warm start the reference controller carried into step t (recorded per step)."""
+    topo = c.topo
+    c.uLin = g["traj_ws_uLin"][t].copy()
+    c.tree = TreeState(topo, c.n, c.d)
+    ps = iter(g["traj_ws_p"][t])
+    for b in range(topo.nbranch):
+        if not topo.is_leaf(b):
+            c.tree.p[b] = next(ps).copy()
+    c.OldInput = g["traj_ws_old"][t].copy()
+
+
+def _check_qp(prob, g, t, label):
+    p = f"s{t}_"
+    for mine, key in ((prob.P, "P"), (prob.A, "A")):
+        ref = coo(g, p + key)
+        assert mine.shape == ref.shape, (label, t, key)
+        diff = abs(mine - ref)
+        assert diff.max() <= 1e-12 * max(1.0, abs(ref).max()), (label, t, key, diff.max())
+    np.testing.assert_allclose(prob.q, g[p + "q"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(np.isfinite(prob.l), np.isfinite(g[p + "l"]))
+    fin = np.isfinite(g[p + "l"])
+    np.testing.assert_allclose(prob.l[fin], g[p + "l"][fin], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(prob.u, g[p + "u"], rtol=1e-12, atol=1e-12)
+
+
+def test_prox_assembly_matches_reference():
+    """BranchMPCProx (quadruped): the reference's OSQP (P, q, A, l, u) rebuilt by the oracle."""
+    from oracle.model import QuadrupedModel, quadruped_policies
+    from oracle.qp_ipm import osqp_like_solve
+    from oracle.tree import ProxController
+    g = golden("quadruped_n25_nb2")
+    for t in (int(k) for k in g["keep"]):
+        mdl = QuadrupedModel(int(g["N"]), float(g["dt"]), quadruped_policies(float(g["v0"])), L1=float(g["L1"]),
+                             W1=float(g["W1"]), L2=float(g["L2"]), W2=float(g["W2"]), col_tol=float(g["col_tol"]))
+        c = ProxController(mdl, int(g["N"]), int(g["NB"]), g["Q"], g["R"], g["dR"], np.zeros((0, 3)), [],
+                           g["Fu"], g["bu"], g["Qslack"], g["xRef0"], solver=osqp_like_solve)
+        if t > 0:
+            _inject_ws(c, g, t)
+        prob = c.setup_problem(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t])
+        _check_qp(prob, g, t, "prox")
+
+
+def test_branch_qp_assembly_matches_reference():
+    """BranchMPC (MPC_branch.py:881, highway): the reference's OSQP problem rebuilt by the oracle."""
+    from oracle.qp_ipm import osqp_like_solve
+    from oracle.tree import BranchQPController
+    g = golden("highway_qp_n8_nb2")
+    for t in (int(k) for k in g["keep"]):
+        mdl = HighwayModel(int(g["N"]), float(g["dt"]), highway_policies(float(g["Kpsi"]), g["traj_lc_target"][t]),
+                           L=float(g["L"]), W=float(g["W"]), s1=float(g["s1"]))
+        c = BranchQPController(mdl, int(g["N"]), int(g["NB"]), g["Q"], g["R"], g["dR"], g["Fx"], g["bx"], g["Fu"],
+                               g["bu"], g["Qslack"], g["xRef0"], solver=osqp_like_solve)
+        if t > 0:
+            _inject_ws(c, g, t)
+        prob = c.setup_problem(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t])
+        _check_qp(prob, g, t, "branch-qp")

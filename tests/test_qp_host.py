@@ -28,3 +28,26 @@ def test_quadruped_prox_replay():
         ref = g[f"s{t}_sol"]
         np.testing.assert_allclose(sol[t], ref, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=f"step {t}")
         np.testing.assert_allclose(r["upred"][t], g[f"s{t}_uPred"], atol=1e-6)
+
+
+def test_branch_mpc_qp_replay():
+    """BranchMPC (MPC_branch.py:881) on the highway scene: every recorded step replayed."""
+    from common import highway_desc_from_golden, highway_policy_rows
+    from bmpc import abi
+    g = golden("highway_qp_n8_nb2")
+    T = len(g["traj_x"])
+    desc = highway_desc_from_golden(g)
+    desc.controller = abi.CTRL_QP
+    hs = H.HostSim(desc, T)
+    hs.set_policies(highway_policy_rows(g["traj_lc_target"], float(g["Kpsi"])))
+    ws_u = np.asarray(g["traj_ws_uLin"], float)
+    warm = ~np.isnan(ws_u).any(axis=(1, 2))
+    hs.set_warm_start(np.nan_to_num(ws_u), np.nan_to_num(g["traj_ws_p"]), None, g["traj_ws_old"])
+    hs.reset_mask(~warm)
+    r = hs.solve(g["traj_x"], g["traj_z"], g["traj_xRef"])
+    np.testing.assert_array_equal(r["status"], g["traj_status"])
+    np.testing.assert_allclose(r["upred"][:, 0], g["traj_u"], atol=1e-6)
+    sol = hs.tree()["sol"]
+    for t in (int(k) for k in g["keep"]):
+        ref = g[f"s{t}_sol"]
+        np.testing.assert_allclose(sol[t], ref, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=f"step {t}")

@@ -187,6 +187,61 @@ def gen_highway(name, N, NB, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+def gen_highway_qp(name, N, NB, steps, keep, out):
+    """main_branch.py's overtake scene with the (commented-out) ``BranchMPC`` controller
+    (main_branch.py:46; the active class definition is MPC_branch.py:881)."""
+    import Init_MPC
+    import MPC_branch
+    from utils import Branch_constants
+
+    n, d, dt, am, rm, N_lane = 4, 2, 0.1, 6.0, 0.3, 4
+    xRef0 = np.array([0.5, 1.8, 15, 0])
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
+                            s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
+    mpc = MPC_branch.BranchMPC(param, model)
+    CURRENT["mpc"] = mpc
+    env = HighwayOvertake(mpc, model, N_lane=N_lane, L=cons.L, W=cons.W, Kpsi=cons.Kpsi,
+                          lc_target0=xRef0, dt=dt)
+    d_out = dict(N=N, NB=NB, m=3, n=n, d=d, dt=dt, am=am, rm=rm, N_lane=N_lane,
+                 L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef0,
+                 Q=param.Q, R=param.R, dR=param.dR, Fx=param.Fx, bx=np.asarray(param.bx, float).reshape(-1),
+                 Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "status", "collision", "ws_uLin", "ws_p", "ws_old")}
+    for t in range(steps):
+        if not env.collision:
+            env.check_collision()
+        traj["ws_uLin"].append(None if mpc.uLin is None else np.array(mpc.uLin, float).copy())
+        traj["ws_p"].append(None if mpc.BT is None else
+                            np.array([np.ravel(b.p) for b in mpc.ndx if b.depth < NB], float))
+        traj["ws_old"].append(np.array(mpc.OldInput, float).reshape(-1).copy())
+        r = env.step(t)
+        prob, sol, info, kw = CURRENT["captured"]
+        assert kw == {"verbose": False, "polish": True}, kw
+        for k in ("x", "z", "xRef", "u", "lc_target"):
+            traj[k].append(r[k])
+        traj["status"].append(info["status_val"])
+        traj["collision"].append(env.collision)
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.P, p + "P", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "q"], d_out[p + "l"], d_out[p + "u"] = prob.q, prob.l, prob.u
+            d_out[p + "sol"] = sol
+            d_out[p + "uPred"], d_out[p + "xPred"] = mpc.uPred, mpc.xPred
+            xs, zs, us, ws = bt_arrays(mpc)
+            d_out[p + "bt_x"], d_out[p + "bt_z"], d_out[p + "bt_u"], d_out[p + "bt_w"] = xs, zs, us, ws
+        print(f"[{name}] t={t:3d} status={info['status_val']} it={info['iter']} u0={mpc.uPred[0]}", flush=True)
+    for k in ("ws_uLin", "ws_p"):
+        shape = next(v.shape for v in traj[k] if v is not None)
+        traj[k] = [np.full(shape, np.nan) if v is None else v for v in traj[k]]
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def gen_quadruped(name, steps, keep, out):
     import Init_MPC
     import MPC_branch
@@ -272,6 +327,7 @@ def main():
         "highway_n8_nb2": lambda: gen_highway("highway_n8_nb2", 8, 2, 5 if a.quick else 40, {0, 1, 2, 30}, out),
         "highway_n10_nb1": lambda: gen_highway("highway_n10_nb1", 10, 1, 5 if a.quick else 20, {0, 1}, out),
         "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 2, {0, 1}, out),
+        "highway_qp_n8_nb2": lambda: gen_highway_qp("highway_qp_n8_nb2", 8, 2, 5 if a.quick else 30, {0, 1, 2, 15}, out),
         "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
     }
     for k, f in jobs.items():
