@@ -53,6 +53,29 @@ def cpu_baseline(N, NB, sample, procs):
                 per_solve_s=float(np.mean([r for r in res])))
 
 
+def cpu_cxx_baseline(N, NB, sample, threads):
+    """The kernel's own algorithm compiled for the host (tests/hostsim, g++ -O2 -fopenmp),
+    OpenMP over `threads` host cores: SURVEY 8(d) CPU baseline (ii).  Two closed-loop steps
+    (cold + warm) of the first `sample` egos of the seeded population."""
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import hostsim_lib as H
+    from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch
+    x, z, xref, tgt = seeded_batch(sample, seed=0)
+    hs = H.HostSim(highway_desc(N=N, NB=NB), sample)
+    hs.set_policies(highway_policy_rows(tgt))
+    t0 = time.time()
+    for _ in range(2):
+        r = hs.solve(x, z, xref)
+        u0 = r["upred"][:, 0]
+        x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
+        z = z + 0.1 * np.stack([z[:, 2] * np.cos(z[:, 3]), z[:, 2] * np.sin(z[:, 3]), 0 * z[:, 0], 0 * z[:, 0]], 1)
+    dt = time.time() - t0
+    return dict(value=round(2 * sample / dt, 2), unit="solves/s", cores=threads, kind="port",
+                sample=f"{sample} seeded egos x 2 closed-loop steps (cold + warm), the kernel algorithm built "
+                       f"for the host (g++ -O2 -fopenmp, {threads} threads), {dt:.1f} s")
+
+
 def _worker_init():
     os.environ["OMP_NUM_THREADS"] = "1"
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
@@ -266,6 +289,10 @@ def main():
             procs = max(1, min(8, len(os.sched_getaffinity(0))))
             cb = cpu_baseline(a.N, a.NB, a.cpu_sample, procs)
             out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+            try:
+                out["cpu_cxx_baseline"] = cpu_cxx_baseline(a.N, a.NB, 1024, max(1, min(16, len(os.sched_getaffinity(0)))))
+            except Exception as exc:   # the C++ host build is a secondary figure only
+                out["cpu_cxx_baseline"] = {"error": str(exc)[:200]}
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -93,9 +93,13 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   HS* h = (HS*)p;
   const Plan& P = h->hp.plan;
   const Layout& L = h->hp.lay;
+  // egos are independent: one OpenMP thread per ego slice (OMP_NUM_THREADS; 1 without -fopenmp)
+#pragma omp parallel
+  {
   HostExec ex;
   std::vector<double> lds(P.nlds);
   ex.lds = lds.data();
+#pragma omp for schedule(dynamic, 4)
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;
@@ -110,6 +114,7 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
     if (J) J[e] = P.desc.controller != BMPC_CTRL_CVAR ? r.pcost : ws[L.sol + P.oJ];
     if (status) status[e] = r.exit_flag;
     if (iters) iters[e] = r.iters;
+  }
   }
   return 0;
 }

@@ -28,7 +28,7 @@ HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc
 def build(force=False):
     newest = max(os.path.getmtime(p) for p in SRCS + HDRS + [os.path.join(REPO, "include", "bmpc.h")])
     if force or not os.path.exists(SO) or os.path.getmtime(SO) < newest:
-        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas",
+        cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fopenmp", "-Wno-unknown-pragmas",
                "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", SO]
         subprocess.check_call(cmd)
     return SO

@@ -25,6 +25,9 @@ for step in range(4):
     print(f"step {step}: wall {1e3 * (t1 - t0):.1f} ms  tree {tm['tree_ms']:.2f} ms  ipm {tm['ipm_ms']:.2f} ms  "
           f"status {np.unique(r['status'], return_counts=True)}  iters {r['iters'].mean():.1f}  "
           f"solves/s {B / (t1 - t0):.0f}", flush=True)
+    its = r["iters"]
+    print("   iters percentiles 50/90/99/max:", np.percentile(its, [50, 90, 99]), its.max(),
+          " histogram >=30:", int((its >= 30).sum()), ">=50:", int((its >= 50).sum()), "==100:", int((its >= 100).sum()))
     u0 = r["upred"][:, 0]
     x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
     z = z + 0.1 * np.stack([z[:, 2], 0 * z[:, 0], 0 * z[:, 0], 0 * z[:, 0]], 1)
