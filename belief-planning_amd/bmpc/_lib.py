@@ -72,6 +72,7 @@ _SIGS = {
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),
+    "bmpc_hmm_eval": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 9),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -145,3 +145,18 @@ def model_eval(desc: abi.PlanDesc, pol_rows, x, u, z, device: int = 0):
                                 *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh"))),
           "bmpc_model_eval")
     return out
+
+
+def hmm_eval(M, m, consts, xb, u, xbackup, device: int = 0):
+    """Batched HMM belief-model linearisation on the GPU (HMM_backup_dyn.py:216-276).
+    consts = (dt, L, W, ylb, yub, col_alpha, s1, tran_diag)."""
+    xb = np.ascontiguousarray(np.atleast_2d(np.asarray(xb, np.float64)))
+    B, nb = xb.shape[0], 4 + M * m
+    u = np.ascontiguousarray(np.broadcast_to(np.atleast_2d(np.asarray(u, np.float64)), (B, 2)))
+    xbk = np.ascontiguousarray(np.broadcast_to(np.asarray(xbackup, np.float64).reshape(-1, M * m, 4), (B, M * m, 4)))
+    hc = np.ascontiguousarray(np.asarray(consts, np.float64).reshape(8))
+    out = dict(xbp=np.zeros((B, nb)), A=np.zeros((B, nb, nb)), B=np.zeros((B, nb, 2)), C=np.zeros((B, nb)),
+               h0=np.zeros((B, M, m)), Jh=np.zeros((B, M, m, nb)))
+    check(lib().bmpc_hmm_eval(context(device), M, m, _p(hc), B, _p(xb), _p(u), _p(xbk),
+                              *(_p(out[k]) for k in ("xbp", "A", "B", "C", "h0", "Jh"))), "bmpc_hmm_eval")
+    return out

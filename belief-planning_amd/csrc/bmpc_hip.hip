@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "bmpc_plan.h"
+#include "bmpc_hmm.h"
 #include "bmpc_qp.h"
 #include "bmpc_solve.h"
 
@@ -184,6 +185,18 @@ __global__ void k_model(bmpc_plan_desc D, const bmpc_policy* pol, int B, const d
   model_eval_point<M>(D, pol + (size_t)b * m, x + b * n, u + b * d, z + b * n, OFF(A, n * n),
                       OFF(Bm, n * d), OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),
                       OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n));
+#undef OFF
+}
+
+__global__ void k_hmm(int M, int m, const double* __restrict__ hc, int B, const double* xb, const double* u,
+                      const double* xbackup, double* xbp, double* A, double* Bm, double* C, double* h0,
+                      double* Jh) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= B) return;
+  const int nb = 4 + M * m;
+#define OFF(ptr, k) (ptr ? ptr + (size_t)p * (k) : nullptr)
+  hmm_linearize(M, m, hc, xb + (size_t)p * nb, u + (size_t)p * 2, xbackup + (size_t)p * M * m * 4, OFF(xbp, nb),
+                OFF(A, nb * nb), OFF(Bm, nb * 2), OFF(C, nb), OFF(h0, M * m), OFF(Jh, M * m * nb));
 #undef OFF
 }
 
@@ -592,6 +605,45 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
     if (hosts[i] && dev[i]) HIPCHECK(hipMemcpy(hosts[i], dev[i], sizeof(double) * B * sizes[i], hipMemcpyDeviceToHost));
   hipFree(buf);
   hipFree(dpol);
+  return 0;
+}
+
+
+int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const double* xb, const double* u,
+                  const double* xbackup, double* xbp, double* A, double* Bm, double* C, double* h0,
+                  double* Jh) {
+  if (!ctx || !hc || !xb || !u || !xbackup || B <= 0) return fail(-22, "null argument");
+  if (M < 1 || m < 1 || M > HMM_MAX_AGENTS || m > HMM_MAX_BACKUPS) return fail(-22, "M, m must be in 1..4");
+  HIPCHECK(hipSetDevice(ctx->device));
+  const size_t nb = 4 + (size_t)M * m;
+  const size_t in_sz[] = {8, (size_t)B * nb, (size_t)B * 2, (size_t)B * M * m * 4};
+  const double* in_h[] = {hc, xb, u, xbackup};
+  const size_t out_sz[] = {nb, nb * nb, nb * 2, nb, (size_t)M * m, (size_t)M * m * nb};
+  double* out_h[] = {xbp, A, Bm, C, h0, Jh};
+  size_t tot = 0;
+  for (size_t v : in_sz) tot += v;
+  for (size_t v : out_sz) tot += (size_t)B * v;
+  double* buf = nullptr;
+  HIPCHECK(hipMalloc(&buf, tot * sizeof(double)));
+  double* cur = buf;
+  double* din[4];
+  for (int i = 0; i < 4; ++i) {
+    din[i] = cur;
+    HIPCHECK(hipMemcpy(cur, in_h[i], in_sz[i] * sizeof(double), hipMemcpyHostToDevice));
+    cur += in_sz[i];
+  }
+  double* dout[6];
+  for (int i = 0; i < 6; ++i) {
+    dout[i] = out_h[i] ? cur : nullptr;
+    cur += (size_t)B * out_sz[i];
+  }
+  hipLaunchKernelGGL(k_hmm, dim3((B + 63) / 64), dim3(64), 0, 0, M, m, din[0], B, din[1], din[2], din[3], dout[0],
+                     dout[1], dout[2], dout[3], dout[4], dout[5]);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipDeviceSynchronize());
+  for (int i = 0; i < 6; ++i)
+    if (out_h[i]) HIPCHECK(hipMemcpy(out_h[i], dout[i], (size_t)B * out_sz[i] * sizeof(double), hipMemcpyDeviceToHost));
+  hipFree(buf);
   return 0;
 }
 

@@ -196,6 +196,18 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
                     double* A, double* Bm, double* C, double* xp, double* p, double* dp,
                     double* zpred, double* h0, double* dh);
 
+/* HMM belief-augmented linearisation, batched over B points: replaces
+ * HMM_backup_dyn.PredictiveModel.regressionAndLinearization (HMM_backup_dyn.py:216-237) of
+ * the graph of calc_xp_expr (:238-276).  M agents (1..4), m backups (1..4), nb = 4 + M*m.
+ *   hc      [8]           {dt, L, W, ylb, yub, col_alpha, s1, tran_diag} (Branch_constants)
+ *   xb      [B][nb]       [x; b stacked column-major] (CasADi reshape, :244)
+ *   u       [B][2]        xbackup [B][M*m][4] (row m*i+j: agent i under backup j)
+ * Outputs (NULL skips): xbp [B][nb], A [B][nb][nb], Bm [B][nb][2], C [B][nb],
+ *   h0 [B][M][m], Jh [B][M][m][nb]   (h0_i = h_i - Jh_i xb, :226-229) */
+int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const double* xb, const double* u,
+                  const double* xbackup, double* xbp, double* A, double* Bm, double* C, double* h0,
+                  double* Jh);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "bmpc_plan.h"
+#include "bmpc_hmm.h"
 #include "bmpc_solve.h"
 
 using namespace bmpc;
@@ -188,6 +189,18 @@ int hs_model_eval(const bmpc_plan_desc* D, const bmpc_policy* pol, int B, const 
                                   OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n));
 #undef OFF
   }
+  return 0;
+}
+
+
+int hs_hmm_eval(int M, int m, const double* hc, int B, const double* xb, const double* u, const double* xbackup,
+                double* xbp, double* A, double* Bm, double* C, double* h0, double* Jh) {
+  const int nb = 4 + M * m;
+  for (int p = 0; p < B; ++p)
+    hmm_linearize(M, m, hc, xb + (size_t)p * nb, u + (size_t)p * 2, xbackup + (size_t)p * M * m * 4,
+                  xbp ? xbp + (size_t)p * nb : nullptr, A ? A + (size_t)p * nb * nb : nullptr,
+                  Bm ? Bm + (size_t)p * nb * 2 : nullptr, C ? C + (size_t)p * nb : nullptr,
+                  h0 ? h0 + (size_t)p * M * m : nullptr, Jh ? Jh + (size_t)p * M * m * nb : nullptr);
   return 0;
 }
 

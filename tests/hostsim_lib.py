@@ -133,3 +133,15 @@ def model_eval(desc, pol_rows, x, u, z):
     lib().hs_model_eval(C.byref(desc), arr, B, _p(x), _p(u), _p(z),
                         *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")))
     return out
+
+
+def hmm_eval(M, m, consts, xb, u, xbackup):
+    xb = np.ascontiguousarray(np.atleast_2d(np.asarray(xb, float)))
+    B, nb = xb.shape[0], 4 + M * m
+    u = np.ascontiguousarray(np.broadcast_to(np.atleast_2d(np.asarray(u, float)), (B, 2)))
+    xbk = np.ascontiguousarray(np.broadcast_to(np.asarray(xbackup, float).reshape(-1, M * m, 4), (B, M * m, 4)))
+    hc = np.ascontiguousarray(np.asarray(consts, float).reshape(8))
+    out = dict(xbp=np.zeros((B, nb)), A=np.zeros((B, nb, nb)), B=np.zeros((B, nb, 2)), C=np.zeros((B, nb)),
+               h0=np.zeros((B, M, m)), Jh=np.zeros((B, M, m, nb)))
+    lib().hs_hmm_eval(M, m, _p(hc), B, _p(xb), _p(u), _p(xbk), *(_p(out[k]) for k in ("xbp", "A", "B", "C", "h0", "Jh")))
+    return out

@@ -178,3 +178,11 @@ def test_branch_mpc_qp_replay_gpu(gpu):
     r = pl.solve(g["traj_x"], g["traj_z"], g["traj_xRef"])
     np.testing.assert_array_equal(r["status"], g["traj_status"])
     np.testing.assert_allclose(r["upred"][:, 0], g["traj_u"], atol=1e-6)
+
+
+def test_hmm_eval_matches_oracle(gpu):
+    """HMM belief linearisation (HMM_backup_dyn.py:216-276) on the GPU vs the oracle, 1e-12."""
+    from test_oracle_hmm import HC, _hmm_case, check_hmm_against_oracle
+    for M, m in ((1, 3), (2, 3), (4, 4)):
+        xb, u, xbk = _hmm_case(M * 10 + m, M, m, 64)
+        check_hmm_against_oracle(gpu.hmm_eval(M, m, HC, xb, u, xbk), M, m, xb, u, xbk)
