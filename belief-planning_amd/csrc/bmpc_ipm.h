@@ -16,6 +16,13 @@
 
 #include "bmpc_tree.h"
 
+#ifndef BMPC_NITREF
+#define BMPC_NITREF 1        // refinement rounds per KKT solve (oracle: 3; 1 keeps parity)
+#endif
+#ifndef BMPC_REFTOL
+#define BMPC_REFTOL 1e-14    // refinement stop: scaled residual <= tol * max(1, |rhs|) (oracle: 1e-14)
+#endif
+
 namespace bmpc {
 
 enum {
@@ -1377,7 +1384,7 @@ BMPC_FN void kkt_solve(const X ex, const Ctx& C, const double* r1, const double*
   const double sc = ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
                                      strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
                                 strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
-  for (int itr = 0; itr < 3; ++itr) {
+  for (int itr = 0; itr < BMPC_NITREF; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     ProfScope _pr(C.ws, L.prof, PROF_REFINE);
 #endif
@@ -1400,7 +1407,7 @@ BMPC_FN void kkt_solve(const X ex, const Ctx& C, const double* r1, const double*
 #ifdef BMPC_HOST_DEBUG
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
-    if (!(err > 1e-14 * fmax(sc, 1.0))) break;
+    if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
     kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
     lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });

@@ -573,7 +573,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
 }
 
 // KKT solve [P E' G'; E 0 0; G 0 -D] [dx; dy; dz] = [r1; r2; r3], D = s/z, with iterative
-// refinement on the D^-1/2-scaled residual (3 rounds, 1e-14 relative; oracle: 1e-15 unscaled)
+// refinement on the D^-1/2-scaled residual (BMPC_NITREF rounds; oracle: 3 rounds, 1e-15 unscaled)
 template <class X, int NX, int NU>
 BMPC_FN void qp_kkt_solve(const X ex, const QpCtx& C, const double* dinv, const double* r1, const double* r2,
                           const double* r3, double* dx, double* dy, double* dz) {
@@ -607,7 +607,7 @@ BMPC_FN void qp_kkt_solve(const X ex, const QpCtx& C, const double* dinv, const 
                                 strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) {
                                   return fabs(r3[i]) * sqrt(dinv[i]);
                                 })));
-  for (int itr = 0; itr < 3; ++itr) {
+  for (int itr = 0; itr < BMPC_NITREF; ++itr) {
     qp_apply_P<X, NX, NU>(ex, C, dx, e1);
     qp_apply_ET<X, NX, NU>(ex, C, dy, tv);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return r1[i] - e1[i] - tv[i]; }, [&](int i, double v) { e1[i] = v; });
@@ -624,7 +624,7 @@ BMPC_FN void qp_kkt_solve(const X ex, const QpCtx& C, const double* dinv, const 
                                    strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) {
                                      return fabs(e3[i]) * sqrt(dinv[i]);
                                    })));
-    if (!(err > 1e-14 * fmax(sc, 1.0))) break;
+    if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
     once(e1, e2, e3, cx, cy, cz);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
     lane_batch<16>(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });
