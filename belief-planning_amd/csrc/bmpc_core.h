@@ -97,7 +97,7 @@ struct Layout {
   // scaling
   size_t dl, eta, wbar, vnt;
   // KKT
-  size_t hx, hu, sd, P, Kg, Luu, kff, lvec, gk, colk, colnu;
+  size_t hx, hu, sd, P, Kg, Luu, kff, lvec, qx0, gk, colk, colnu;
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
   // BranchMPCProx QP: u-rate couplings, linear cost, augmented Riccati P~, [Kx Kv], l~
   size_t qo, qq, Pa, Ka, la;

@@ -865,17 +865,16 @@ BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[N
 // rhs r_i lives in z-space (x, u, S parts at P.oX/oU/oS), e_i in eq-space (first T*n rows;
 // pass Layout::zeros for none).  Solutions go to out_i (z-space tree parts) and nu_i
 // (eq-space, NULL skips).
-// Mapping: one task per (branch, rhs), run by a group of W = X::kTaskLanes lanes (a DPP
-// quad on the GPU); lane gl of the group owns state rows gl*RX .. gl*RX+RX-1 and the slack
-// rows c = gl, gl+W, ...  The backward affine term l and the forward state x are carried
-// in registers along the branch; branches of one depth run in parallel, depths in sequence.
+// Structure: (1) lane-parallel pre-pass: slack elimination of every node's x rhs;
+// (2) the two sequential sweeps, one task per (branch, rhs) run by a group of
+// W = X::kTaskLanes lanes (a DPP quad on the GPU; lane gl owns state rows gl*RX..), carrying
+// the affine term l / the state x in registers along the branch -- only the Riccati data
+// is loaded per node; (3) lane-parallel post-pass: multipliers nu and slack recovery.
 template <class X, int NX, int NU>
 BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r,
                         const double* const* e, double* const* out, double* const* nu) {
   constexpr int W = X::kTaskLanes;
   constexpr int RX = (NX + W - 1) / W;
-  constexpr int MC = BMPC_MAX_FX + 1;
-  constexpr int RC = (MC + W - 1) / W;     // slack rows per lane (upper bound)
   const Plan& P = *C.P;
   const Layout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_TREESOLVE);
@@ -884,13 +883,31 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
   const int Nc = P.Nc;
   double* ws = C.ws;
   double* lv_ = ws + L.lvec;   // [nr][T][NX]
+  double* q0_ = ws + L.qx0;    // [nr][T][NX]
   double* kf_ = ws + L.kff;    // [nr][U][NU]
   const size_t lstr = (size_t)P.T * NX, kstr = (size_t)P.U * NU;
+  const double* dh = ws + L.dh;
+  const double* sdv = ws + L.sd;
   const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
-  // slack-row coefficient f_c[j] (c = 0: -dh_k; c >= 1: Fx[c-1])
-  auto fxc = [&](int c, int j, const double* dhk) { return c == 0 ? -dhk[j] : P.desc.Fx[(c - 1) * NX + j]; };
 
-  // ---- backward sweep (leaves -> root) --------------------------------------------------
+  // ---- (1) pre-pass: qx0 = -r_x - sum_c f_c df r_S / sd (non-terminal nodes) -------------
+  for (int ri = 0; ri < nr; ++ri) {
+    const double* rr = r[ri];
+    double* q0 = q0_ + ri * lstr;
+    lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+      const int k = it / NX, j = it % NX;
+      double v = -rr[P.oX + it];
+      if (t.x_u[k] >= 0)
+        for (int c = 0; c < Nc; ++c) {
+          const double a = sdv[(k * Nc + c) * 2 + 1] * rr[P.oS + k * Nc + c] / sdv[(k * Nc + c) * 2];
+          v -= (c == 0 ? -dh[it] : P.desc.Fx[(c - 1) * NX + j]) * a;
+        }
+      return v;
+    }, [&](int it, double v) { q0[it] = v; });
+  }
+  ex.sync();
+
+  // ---- (2a) backward sweep (leaves -> root) ----------------------------------------------
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
@@ -902,29 +919,29 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
       const double* rr = r[ri];
       const double* ee = e[ri];
       double* lvec = lv_ + ri * lstr;
+      const double* q0 = q0_ + ri * lstr;
       double* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
       const int c0 = t.br_child0[b];
       double l[RX];
-      if (leaf) {   // terminal node: l = -r_x (no input, no slack elimination)
+      if (leaf) {   // terminal node: l = -r_x (= qx0 there)
         const int tn = ndx + len;
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q;
-          l[q] = i < NX ? -rr[P.oX + tn * NX + i] : 0.0;
+          l[q] = i < NX ? q0[tn * NX + i] : 0.0;
           if (i < NX) lvec[tn * NX + i] = l[q];
         }
       }
       for (int jn = len - 1; jn >= 0; --jn) {
         const int k = ndx + jn, u = ndu + jn;
         // ---- loads (independent of the recursion) ----
-        double rx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU], dhk[NX];
-        double rS[RC], sdv[RC], dfv[RC];
+        double qx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU];
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
-          rx[q] = rr[P.oX + k * NX + i];
+          qx[q] = q0[k * NX + i];
 #pragma unroll
           for (int j = 0; j < NX; ++j) Acol[q][j] = ws[L.Ad + u * NX * NX + j * NX + i];
 #pragma unroll
@@ -935,15 +952,6 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
         mat_load(Lu, ws + L.Luu + u * NU * NU);
 #pragma unroll
         for (int m = 0; m < NU; ++m) ru[m] = rr[P.oU + u * NU + m];
-#pragma unroll
-        for (int j = 0; j < NX; ++j) dhk[j] = ws[L.dh + k * NX + j];
-#pragma unroll
-        for (int q = 0; q < RC; ++q) {
-          const int c = gl + q * W < Nc ? gl + q * W : Nc - 1;
-          rS[q] = rr[P.oS + k * Nc + c];
-          sdv[q] = ws[L.sd + (k * Nc + c) * 2];
-          dfv[q] = ws[L.sd + (k * Nc + c) * 2 + 1];
-        }
         // ---- g = sum over successors of (l_c + P_c e_c), own rows ----
         double g[RX];
         if (jn < len - 1 || leaf) {
@@ -981,7 +989,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
           if (gl * RX + q >= NX) g[q] = 0.0;
         double gfull[NX];
         task_gather<NX, RX, W>(ex, g, gfull);
-        // ---- qu = -ru + B'g ----
+        // ---- qu = -ru + B'g ;  kf = -Quu^-1 qu ;  l = qx0 + A'g + K'qu ----
         double qu[NU];
 #pragma unroll
         for (int m = 0; m < NU; ++m) {
@@ -990,23 +998,6 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
           for (int q = 0; q < RX; ++q) v += Brow[q][m] * g[q];
           qu[m] = -ru[m] + ex.tsum(v);
         }
-        // ---- slack elimination sum_c f_c a_c (lane owns slack rows c = gl + q W) ----
-        double sl[NX];
-#pragma unroll
-        for (int j = 0; j < NX; ++j) sl[j] = 0.0;
-#pragma unroll
-        for (int q = 0; q < RC; ++q) {
-          const int c = gl + q * W;
-          if (c < Nc) {
-            const double a = dfv[q] * rS[q] / sdv[q];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) sl[j] += fxc(c, j, dhk) * a;
-          }
-        }
-        double slf[NX];
-#pragma unroll
-        for (int j = 0; j < NX; ++j) slf[j] = ex.tsum(sl[j]);
-        // ---- l_k = -rx - sl + A'g + K'qu ;  kf = -Quu^-1 qu ----
         double kfv[NU];
 #pragma unroll
         for (int m = 0; m < NU; ++m) kfv[m] = -qu[m];
@@ -1014,7 +1005,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q;
-          double v = -rx[q] - slf[i < NX ? i : NX - 1];
+          double v = qx[q];
 #pragma unroll
           for (int j = 0; j < NX; ++j) v += Acol[q][j] * gfull[j];
 #pragma unroll
@@ -1030,7 +1021,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
     ex.sync();
   }
 
-  // ---- forward sweep (root -> leaves) -----------------------------------------------------
+  // ---- (2b) forward sweep (root -> leaves): x and u only ------------------------------------
   for (int it = ex.lane; it < nr; it += ex.nlanes) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) out[it][P.oX + j] = e[it][j];
@@ -1045,10 +1036,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
       if (task >= ntask) continue;
       const int b = b0 + task / nr, ri = task % nr;
       double* o = out[ri];
-      const double* rr = r[ri];
       const double* ee = e[ri];
-      double* nn = nu[ri];
-      const double* lvec = lv_ + ri * lstr;
       const double* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
@@ -1056,63 +1044,24 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
       double xk[NX];      // full state (every lane of the group holds all of it)
 #pragma unroll
       for (int j = 0; j < NX; ++j) xk[j] = o[P.oX + ndx * NX + j];   // written by the parent group
-      const int nnodes = leaf ? len + 1 : len;
-      for (int jn = 0; jn < nnodes; ++jn) {
-        const int k = ndx + jn;
-        const bool term = jn == len;
-        const int u = term ? ndu + len - 1 : ndu + jn;    // (terminal: input loads unused)
+      for (int jn = 0; jn < len; ++jn) {
+        const int k = ndx + jn, u = ndu + jn;
         // ---- loads ----
-        double Prow[RX][NX], lk[RX], Arow[RX][NX], Brow[RX][NU], Kcol[RX][NU], kfu[NU], en[RX], dhk[NX];
-        double rS[RC], sdv[RC], dfv[RC];
+        double Arow[RX][NX], Brow[RX][NU], Kcol[RX][NU], kfu[NU], en[RX];
         const int kn = (jn < len - 1 || leaf) ? k + 1 : t.br_ndx[c0 >= 0 ? c0 : 0];
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
-#pragma unroll
-          for (int j = 0; j < NX; ++j) Prow[q][j] = ws[L.P + k * NX * NX + i * NX + j];
-          lk[q] = lvec[k * NX + i];
 #pragma unroll
           for (int j = 0; j < NX; ++j) Arow[q][j] = ws[L.Ad + u * NX * NX + i * NX + j];
 #pragma unroll
           for (int m = 0; m < NU; ++m) Brow[q][m] = ws[L.Bd + u * NX * NU + i * NU + m];
 #pragma unroll
           for (int m = 0; m < NU; ++m) Kcol[q][m] = ws[L.Kg + u * NU * NX + m * NX + i];
-          en[q] = ee[(term ? k : kn) * NX + i];
+          en[q] = ee[kn * NX + i];
         }
 #pragma unroll
         for (int m = 0; m < NU; ++m) kfu[m] = kf[u * NU + m];
-#pragma unroll
-        for (int j = 0; j < NX; ++j) dhk[j] = ws[L.dh + k * NX + j];
-#pragma unroll
-        for (int q = 0; q < RC; ++q) {
-          const int c = gl + q * W < Nc ? gl + q * W : Nc - 1;
-          rS[q] = rr[P.oS + k * Nc + c];
-          sdv[q] = ws[L.sd + (k * Nc + c) * 2];
-          dfv[q] = ws[L.sd + (k * Nc + c) * 2 + 1];
-        }
-        // ---- nu_k = -(l_k + P_k x_k), own rows ----
-        if (nn)
-#pragma unroll
-          for (int q = 0; q < RX; ++q) {
-            const int i = gl * RX + q;
-            double v = lk[q];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) v += Prow[q][j] * xk[j];
-            if (i < NX) nn[k * NX + i] = -v;
-          }
-        // ---- slack recovery, own slack rows ----
-#pragma unroll
-        for (int q = 0; q < RC; ++q) {
-          const int c = gl + q * W;
-          if (c < Nc) {
-            double fx = 0.0;
-            if (!term)
-#pragma unroll
-              for (int j = 0; j < NX; ++j) fx += fxc(c, j, dhk) * xk[j];
-            o[P.oS + k * Nc + c] = (rS[q] + dfv[q] * fx) / sdv[q];
-          }
-        }
-        if (term) break;
         // ---- u = kf + K x ----
         double uk[NU];
 #pragma unroll
@@ -1158,6 +1107,32 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
     }
     ex.sync();
   }
+
+  // ---- (3) post-pass: nu_k = -(l_k + P_k x_k), slack recovery --------------------------------
+  for (int ri = 0; ri < nr; ++ri) {
+    double* o = out[ri];
+    const double* rr = r[ri];
+    const double* lvec = lv_ + ri * lstr;
+    if (nu[ri]) {
+      double* nn = nu[ri];
+      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+        const int k = it / NX, i = it % NX;
+        double v = lvec[it];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) v += ws[L.P + k * NX * NX + i * NX + j] * o[P.oX + k * NX + j];
+        return -v;
+      }, [&](int it, double v) { nn[it] = v; });
+    }
+    lane_batch<4>(ex, 0, P.T * Nc, [&](int it) {
+      const int k = it / Nc, c = it % Nc;
+      double fx = 0.0;
+      if (t.x_u[k] >= 0)
+#pragma unroll
+        for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * o[P.oX + k * NX + j];
+      return (rr[P.oS + it] + sdv[it * 2 + 1] * fx) / sdv[it * 2];
+    }, [&](int it, double v) { o[P.oS + it] = v; });
+  }
+  ex.sync();
 }
 
 // dense LU with partial pivoting of the coupling system (row-major n x n, in LDS)

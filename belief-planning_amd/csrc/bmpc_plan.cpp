@@ -399,7 +399,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.Kg = take((size_t)U * d * n);
   L.Luu = take((size_t)U * d * d);
   L.kff = take((size_t)(nc > 0 ? nc : 1) * U * d);   // (PROX: one rhs)
-  L.lvec = take((size_t)nc * T * n);
+  L.lvec = take((size_t)(nc > 0 ? nc : 1) * T * n);
+  L.qx0 = take((size_t)(nc > 0 ? nc : 1) * T * n);   // slack-eliminated x rhs of the tree sweeps
   L.gk = take((size_t)nc * nv);
   L.colk = take((size_t)nc * nv);
   L.colnu = take((size_t)nc * neq);
