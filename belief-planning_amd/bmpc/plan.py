@@ -115,11 +115,12 @@ class BatchPlan:
 
     # ---- timing ---------------------------------------------------------------------------
     PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
-              "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree")
+              "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree", "G_lp", "G_cone", "napplyG",
+              "x1", "x2", "x3", "x4")
 
     def counters(self):
         """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build)."""
-        out = np.zeros((self.batch, 16))
+        out = np.zeros((self.batch, 24))
         check(lib().bmpc_get_counters(self._h, _p(out)), "bmpc_get_counters")
         return out
 

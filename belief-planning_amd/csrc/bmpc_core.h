@@ -28,6 +28,46 @@
 namespace bmpc {
 
 // ------------------------------------------------------------------------------------
+// address-space / uniformity hints for out-of-line device functions.  Arguments of a
+// non-kernel function arrive as generic, lane-varying pointers: every load through them is a
+// flat_load (counted by both vmcnt and lgkmcnt, so waits for LDS or scalar data also wait for
+// HBM) and every Plan field is a vector load queued behind the wave's HBM misses.
+//   gmem(p)  -- p points to global memory: loads through it become global_load
+//   uconst(p) -- p is wave-uniform and the pointee is read-only for the kernel: loads with
+//               uniform offsets become s_load (scalar cache, lgkmcnt only)
+//   uglob(p) -- wave-uniform global pointer (the ego workspace)
+// On the host build these are the identity.
+// ------------------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+__device__ __forceinline__ T* rfl_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<T*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+template <class T>
+__device__ __forceinline__ T* gmem(T* p) {
+  return (T*)(__attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ const T* uconst(const T* p) {
+  return (const T*)(const __attribute__((address_space(4))) T*)rfl_ptr(p);
+}
+template <class T>
+__device__ __forceinline__ T* uglob(T* p) {
+  return gmem(rfl_ptr(p));
+}
+#else
+template <class T>
+inline T* gmem(T* p) { return p; }
+template <class T>
+inline const T* uconst(const T* p) { return p; }
+template <class T>
+inline T* uglob(T* p) { return p; }
+#endif
+
+// ------------------------------------------------------------------------------------
 // Plan: per-plan constants and topology tables (shared by every ego of the batch).
 // ------------------------------------------------------------------------------------
 struct Topo {
@@ -114,7 +154,7 @@ enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */ };
 enum {
   PROF_TREE = 0, PROF_RESID, PROF_SCALING, PROF_FACTOR, PROF_COUPLING, PROF_KKT, PROF_TREESOLVE,
   PROF_REFINE, PROF_STEP, PROF_INIT, PROF_TOTAL, PROF_NSOLVE, PROF_APPLYW, PROF_APPLYG, PROF_APPLYGT,
-  PROF_NTREE, PROF_COUNT = 16
+  PROF_NTREE, PROF_G_LP, PROF_G_CONE, PROF_NAPPLYG, PROF_X1, PROF_X2, PROF_X3, PROF_X4, PROF_COUNT = 24
 };
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {

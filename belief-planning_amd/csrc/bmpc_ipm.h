@@ -93,21 +93,25 @@ template <class X, int NX, int NU>
 BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
   const Plan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
+  BMPC_COUNT(C.ws, *C.L, PROF_NAPPLYG);
+  BMPC_TIC(t_glp);
   const Topo& t = P.t;
   const int Nc = P.Nc;
   const double* dh = C.at(C.L->dh);
   // Fx rows + positivity rows
   struct Two { double a, b; };
+  // branch-free bodies: every load of a batch is issued before the first wait (a branch on
+  // a loaded topology index would serialise the batch into one round trip per element)
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     const double S = zv[P.oS + it];
+    const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
+    const int cr = c > 0 ? c - 1 : 0;
     double v = -S;
-    if (t.x_u[k] >= 0) {
 #pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        const double f = c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j];
-        v += f * zv[P.oX + k * NX + j];
-      }
+    for (int j = 0; j < NX; ++j) {
+      const double fd = dh[k * NX + j], fx = P.desc.Fx[cr * NX + j];
+      v += (on * (c == 0 ? -fd : fx)) * zv[P.oX + k * NX + j];
     }
     return Two{v, -S};
   }, [&](int it, Two r) { out[P.rFx + it] = r.a; out[P.rPos + it] = r.b; });
@@ -125,33 +129,42 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
   }, [&](int it, double v) { out[P.rRisk + it] = v; });
   const double* boost = C.at(C.L->boost);
   const double Qs = P.desc.Qslack[1];
+  BMPC_TOC(C.ws, *C.L, PROF_G_LP, t_glp);
+  BMPC_TIC(t_gcone);
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
-    const int c = k >= 0 ? t.cone_c[k] : -1;
-    // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node
+    // topology of the cone, loaded together (clamped indices, no branch on loaded values)
+    const int kk = k >= 0 ? k : 0;
+    const int c = k >= 0 ? t.cone_c[kk] : -1;
+    const int cb = t.cone_b[kk], ci = t.cone_i[kk];
+    const double ebst = exp(-boost[kk]);
+    const int c0 = c >= 0 ? c : 0;
+    const int ndx = t.br_ndx[c0], ndu = t.br_ndu[c0];
+    const bool hasch = t.br_child0[c0] >= 0;
+    // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node; the
+    // group's lane 0 folds the risk-variable terms into its partial
     {
-      const int ndx = c >= 0 ? t.br_ndx[c] : 0;
+      // the root cone (c < 0) holds the root node's slacks only (ndx = br_ndx[0] = 0)
       const int nn = c >= 0 ? P.N : (k >= 0 ? 1 : 0);
+      const double xon = c >= 0 ? -2.0 : 0.0;
       double part = strided_partial<4>(G.gl, G.cg, nn, [&](int j) {
         double a = 0.0;
-        if (c >= 0) {
 #pragma unroll
-          for (int r2 = 0; r2 < NX; ++r2) a += -2.0 * C.qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
-        }
+        for (int r2 = 0; r2 < NX; ++r2) a += xon * C.qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
         for (int cc = 0; cc < P.Nc; ++cc) a += Qs * zv[P.oS + (ndx + j) * P.Nc + cc];
         return a;
       });
-      const double f1 = ex.gsum(part, G.cg);
       if (k >= 0 && G.gl == 0) {
-        double acc = f1;
         if (c >= 0) {
-          const int b = t.cone_b[k], i = t.cone_i[k];
-          acc += zv[P.oSig + b] + zv[P.oMup + b + i] - zv[P.oMum + b + i];
-          if (t.br_child0[c] >= 0) acc += zv[P.oRho + c];
+          double acc = zv[P.oSig + cb] + zv[P.oMup + cb + ci] - zv[P.oMum + cb + ci];
+          if (hasch) acc += zv[P.oRho + c];
+          part += acc;
         } else {
-          acc += -zv[P.oJ] + zv[P.oRho + 0];
+          part += -zv[P.oJ] + zv[P.oRho + 0];
         }
-        const double f = acc * exp(-boost[k]);
+      }
+      const double f = ex.gsum(part, G.cg) * ebst;
+      if (k >= 0 && G.gl == 0) {
         out[off] = f;
         out[off + q - 1] = -f;
       }
@@ -163,19 +176,20 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
       double v = 0.0;
       if (it < nxn) {
         const int j = it / NX, r = it % NX;
-        const int xk = t.br_ndx[c] + j;
+        const int xk = ndx + j;
 #pragma unroll
         for (int s2 = 0; s2 < NX; ++s2) v += -2.0 * P.W1[r * NX + s2] * zv[P.oX + xk * NX + s2];
       } else {
         const int jj = it - nxn;
         const int j = jj / NU, r = jj % NU;
-        const int uk = c >= 0 ? t.br_ndu[c] + j : 0;
+        const int uk = c >= 0 ? ndu + j : 0;
 #pragma unroll
         for (int s2 = 0; s2 < NU; ++s2) v += -2.0 * P.Wu[r * NU + s2] * zv[P.oU + uk * NU + s2];
       }
       return v;
     }, [&](int it, double v) { out[off + 1 + it] = v; });
   }
+  BMPC_TOC(C.ws, *C.L, PROF_G_CONE, t_gcone);
   ex.sync();
 }
 

@@ -180,7 +180,7 @@ int bmpc_get_tree(bmpc_plan* plan, double* xbar, double* ubar, double* zbar, dou
 int bmpc_enable_timing(bmpc_plan* plan, int on);
 int bmpc_timing(bmpc_plan* plan, double* ms /* [2] */, int32_t* count);
 
-/* Per-ego phase cycle counters [batch][16] (s_memtime cycles accumulated since plan
+/* Per-ego phase cycle counters [batch][24] (s_memtime cycles accumulated since plan
  * creation: tree, residuals, scaling, factor, coupling, kkt, tree-solve, refine, -, init,
  * total, kkt-solve count).  All zero unless the library was built with -DBMPC_PROFILE. */
 int bmpc_get_counters(bmpc_plan* plan, double* out);

@@ -40,6 +40,9 @@ def main():
         v = c[:, i].mean()
         print(f"{name:>10s} {v/1e6:10.3f} {100*v/max(tot,1):8.1f} {v/max(it.mean(),1)/1e3:10.1f}")
     print(f"probe: one dependent global load = {c[:, 8].mean() / (it.mean() + 1):.0f} cycles")
+    ng = c[:, 18].mean()
+    print(f"apply_G calls/iter {ng/it.mean():.2f}: per call total {c[:, 13].mean()/max(ng,1):.0f} "
+          f"LP {c[:, 16].mean()/max(ng,1):.0f} cones {c[:, 17].mean()/max(ng,1):.0f} cycles")
     ns, nt = c[:, 11].mean(), c[:, 15].mean()
     print(f"kkt solves/ego {ns:.1f} ({ns/it.mean():.2f}/iter), tree solves/ego {nt:.1f} ({nt/it.mean():.2f}/iter); "
           f"cycles per tree solve {c[:, 6].mean()/max(nt,1):.0f}, per kkt solve {c[:, 5].mean()/max(ns,1):.0f}")
