@@ -28,75 +28,71 @@
 namespace bmpc {
 
 // ------------------------------------------------------------------------------------
-// address-space / uniformity hints for out-of-line device functions.  Arguments of a
-// non-kernel function arrive as generic, lane-varying pointers: every load through them is a
-// flat_load (counted by both vmcnt and lgkmcnt, so waits for LDS or scalar data also wait for
-// HBM) and every Plan field is a vector load queued behind the wave's HBM misses.
-//   gmem(p)  -- p points to global memory: loads through it become global_load
-//   uconst(p) -- p is wave-uniform and the pointee is read-only for the kernel: loads with
-//               uniform offsets become s_load (scalar cache, lgkmcnt only)
-//   uglob(p) -- wave-uniform global pointer (the ego workspace)
-// On the host build these are the identity.
+// Address spaces.  Arguments of an out-of-line device function arrive as generic,
+// lane-varying pointers: every load through them is a flat_load (counted by both vmcnt and
+// lgkmcnt, so a wait for LDS or scalar data also waits for HBM) and every Plan field is a
+// vector load queued behind the wave's HBM misses.  The device code therefore types its
+// pointers: the ego workspace and the plan's topology tables are global memory (gdouble,
+// gint), the Plan / Layout are constant memory read with wave-uniform addresses (s_load
+// through the scalar cache), the per-wave scratch is LDS (ldouble).  On the host build the
+// qualifiers vanish.
 // ------------------------------------------------------------------------------------
 #if defined(__HIP_DEVICE_COMPILE__)
+#define BMPC_AS_GLOBAL __attribute__((address_space(1)))
+#define BMPC_AS_LDS __attribute__((address_space(3)))
+#define BMPC_AS_CONST __attribute__((address_space(4)))
+#else
+#define BMPC_AS_GLOBAL
+#define BMPC_AS_LDS
+#define BMPC_AS_CONST
+#endif
+typedef BMPC_AS_GLOBAL double gdouble;
+typedef BMPC_AS_LDS double ldouble;
+typedef const BMPC_AS_GLOBAL int32_t gint;
+
+// the value of a wave-uniform pointer held in a VGPR, moved to SGPRs
 template <class T>
-__device__ __forceinline__ T* rfl_ptr(T* p) {
+BMPC_HD T* uniform_ptr(T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   return reinterpret_cast<T*>((static_cast<uint64_t>(hi) << 32) | lo);
-}
-template <class T>
-__device__ __forceinline__ T* gmem(T* p) {
-  return (T*)(__attribute__((address_space(1))) T*)p;
-}
-template <class T>
-__device__ __forceinline__ const T* uconst(const T* p) {
-  return (const T*)(const __attribute__((address_space(4))) T*)rfl_ptr(p);
-}
-template <class T>
-__device__ __forceinline__ T* uglob(T* p) {
-  return gmem(rfl_ptr(p));
-}
 #else
-template <class T>
-inline T* gmem(T* p) { return p; }
-template <class T>
-inline const T* uconst(const T* p) { return p; }
-template <class T>
-inline T* uglob(T* p) { return p; }
+  return p;
 #endif
+}
 
 // ------------------------------------------------------------------------------------
 // Plan: per-plan constants and topology tables (shared by every ego of the batch).
 // ------------------------------------------------------------------------------------
 struct Topo {
   // per branch (BFS order of MPC_branch.inittree)
-  const int32_t* br_depth;
-  const int32_t* br_len;
-  const int32_t* br_ndx;
-  const int32_t* br_ndu;
-  const int32_t* br_child0;   // first child (children are contiguous), -1 for leaves
+  gint* br_depth;
+  gint* br_len;
+  gint* br_ndx;
+  gint* br_ndu;
+  gint* br_child0;   // first child (children are contiguous), -1 for leaves
   // per x node
-  const int32_t* x_u;         // u node of x node (-1 for leaf terminal nodes)
-  const int32_t* x_srcu;      // u node whose (A,B,C) defines this node (-1 for root)
-  const int32_t* x_srcx;      // x node of that source
-  const int32_t* x_cone;      // cone whose middle rows contain x (-1 none)
-  const int32_t* x_conepos;   // position j of the node inside the cone's branch
-  const int32_t* x_branch;
-  const int32_t* succ_off;    // CSR successors of each x node: nodes defined by its (A,B,C)
-  const int32_t* succ;
-  const int32_t* lvl_off;     // x nodes grouped by tree level (root = level 0)
-  const int32_t* lvl_nodes;
+  gint* x_u;         // u node of x node (-1 for leaf terminal nodes)
+  gint* x_srcu;      // u node whose (A,B,C) defines this node (-1 for root)
+  gint* x_srcx;      // x node of that source
+  gint* x_cone;      // cone whose middle rows contain x (-1 none)
+  gint* x_conepos;   // position j of the node inside the cone's branch
+  gint* x_branch;
+  gint* succ_off;    // CSR successors of each x node: nodes defined by its (A,B,C)
+  gint* succ;
+  gint* lvl_off;     // x nodes grouped by tree level (root = level 0)
+  gint* lvl_nodes;
   // per u node
-  const int32_t* u_x;
-  const int32_t* u_cone;
+  gint* u_x;
+  gint* u_cone;
   // per cone
-  const int32_t* cone_b;      // parent non-leaf branch index (-1 = root cone)
-  const int32_t* cone_i;      // child slot i
-  const int32_t* cone_c;      // child branch (-1 = root cone)
-  const int32_t* cone_q;      // cone dimension
-  const int32_t* cone_off;    // first row of the cone in the conic row vector
+  gint* cone_b;      // parent non-leaf branch index (-1 = root cone)
+  gint* cone_i;      // child slot i
+  gint* cone_c;      // child branch (-1 = root cone)
+  gint* cone_q;      // cone dimension
+  gint* cone_off;    // first row of the cone in the conic row vector
 };
 
 struct Plan {
@@ -144,6 +140,9 @@ struct Layout {
   size_t stride;  // doubles per ego
 };
 
+typedef const BMPC_AS_CONST Plan CPlan;
+typedef const BMPC_AS_CONST Layout CLayout;
+
 // misc slots
 enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */ };
 
@@ -158,9 +157,10 @@ enum {
 };
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {
-  double* slot;
+  gdouble* slot;
   long long t0;
-  __device__ ProfScope(double* ws, size_t base, int id) : slot(ws + base + id), t0(__builtin_amdgcn_s_memtime()) {}
+  template <class PT>
+  __device__ ProfScope(PT ws, size_t base, int id) : slot((gdouble*)(ws + base + id)), t0(__builtin_amdgcn_s_memtime()) {}
   __device__ ~ProfScope() {
     const long long t1 = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) *slot += (double)(t1 - t0);
@@ -261,16 +261,16 @@ BMPC_HD ConeGroups cone_groups(const X& ex, int cgrp, int ncones) {
 // ------------------------------------------------------------------------------------
 // small dense helpers (row-major, compile-time sizes)
 // ------------------------------------------------------------------------------------
-template <int R, int C>
-BMPC_HD void mat_load(double (&M)[R][C], const double* p) {
+template <int R, int C, class PT>
+BMPC_HD void mat_load(double (&M)[R][C], PT p) {
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll
     for (int j = 0; j < C; ++j) M[i][j] = p[i * C + j];
 }
 
-template <int R, int C>
-BMPC_HD void mat_store(const double (&M)[R][C], double* p) {
+template <int R, int C, class PT>
+BMPC_HD void mat_store(const double (&M)[R][C], PT p) {
 #pragma unroll
   for (int i = 0; i < R; ++i)
 #pragma unroll

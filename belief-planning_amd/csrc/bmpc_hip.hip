@@ -34,7 +34,7 @@ __device__ __forceinline__ double dpp_d(double v) {
 
 struct DevExec {
   int lane;
-  double* lds;   // this wave's LDS scratch (Plan::nlds doubles; k_ipm only)
+  ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm only)
   static constexpr int nlanes = 64;
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  DevExec ex{(int)threadIdx.x, lds_dyn};
+  DevExec ex{(int)threadIdx.x, (ldouble*)lds_dyn};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_ipm<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  DevExec ex{(int)threadIdx.x, lds_dyn};
+  DevExec ex{(int)threadIdx.x, (ldouble*)lds_dyn};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_qp<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;

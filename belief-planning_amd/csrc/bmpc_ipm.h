@@ -34,14 +34,30 @@ enum {
 // context bundling the per-ego pointers
 // ------------------------------------------------------------------------------------
 struct Ctx {
-  const Plan* P;
-  const Layout* L;
-  double* ws;
-  double qx[BMPC_MAX_N];   // xRef' Q
-  double jcons;            // frozen xRef'Q xRef of the first solve (:1939)
-  double ralpha;
-  BMPC_HD double* at(size_t off) const { return ws + off; }
+  CPlan* P;
+  CLayout* L;
+  gdouble* ws;
+  BMPC_HD gdouble* at(size_t off) const { return ws + off; }
+  // the same context with its pointers in SGPRs (first statement of every out-of-line phase)
+  BMPC_HD Ctx uniform() const { return Ctx{uniform_ptr(P), uniform_ptr(L), uniform_ptr(ws)}; }
 };
+
+// xRef' Q (the cone rows' linear cost term, MPC_branch.py:1927-1940); xref is written by the
+// tree kernel, Q is plan constant
+template <int NX>
+BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
+  const gdouble* xref = C.at(C.L->xref);
+  double xr[NX];
+#pragma unroll
+  for (int r = 0; r < NX; ++r) xr[r] = xref[r];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) {
+    double v = 0.0;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) v += xr[r] * C.P->desc.Q[r * NX + c];
+    qx[c] = v;
+  }
+}
 
 // cone-group rounds (see ConeGroups): G, and per round k / off / q of the owned cone
 #define BMPC_CONE_ROUNDS(ex, P, G)                                \
@@ -57,13 +73,13 @@ struct Ctx {
 // idle member (k < 0, q = 0): every lane of the wave must make the same calls.
 // ------------------------------------------------------------------------------------
 template <class X>
-BMPC_HD double cone_dot(const X ex, const ConeGroups& G, const double* a, const double* b, int off, int q) {
+BMPC_HD double cone_dot(const X ex, const ConeGroups& G, const gdouble* a, const gdouble* b, int off, int q) {
   return ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) { return a[off + i] * b[off + i]; }), G.cg);
 }
 
 // v0^2 - ||v1||^2 without squaring the dominant entry (see oracle.ecos_ipm.cone_res)
 template <class X>
-BMPC_HD double cone_res(const X ex, const ConeGroups& G, const double* v, int off, int q) {
+BMPC_HD double cone_res(const X ex, const ConeGroups& G, const gdouble* v, int off, int q) {
   double amax = 0.0, aidx = 1e300;
   for (int i = 1 + G.gl; i < q; i += G.cg) {
     const double a = fabs(v[off + i]);
@@ -83,21 +99,24 @@ BMPC_HD double cone_res(const X ex, const ConeGroups& G, const double* v, int of
 // ------------------------------------------------------------------------------------
 // x-coefficients of LP row c of state node k: c = 0 -> -dh_k, c >= 1 -> Fx[c-1]
 BMPC_HD double fx_coef(const Ctx& C, int k, int c, int j) {
-  const Plan& P = *C.P;
+  CPlan& P = *C.P;
   if (c == 0) return -C.ws[C.L->dh + k * P.n + j];
   return P.desc.Fx[(c - 1) * P.n + j];
 }
 
 // out(rows) = G zv, cone rows boosted
 template <class X, int NX, int NU>
-BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
-  const Plan& P = *C.P;
+BMPC_FN void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out) {
+  const Ctx C = Cin.uniform();
+  double qx[NX];
+  ctx_qx<NX>(C, qx);
+  CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
   BMPC_COUNT(C.ws, *C.L, PROF_NAPPLYG);
   BMPC_TIC(t_glp);
-  const Topo& t = P.t;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  const double* dh = C.at(C.L->dh);
+  const gdouble* dh = C.at(C.L->dh);
   // Fx rows + positivity rows
   struct Two { double a, b; };
   // branch-free bodies: every load of a batch is issued before the first wait (a branch on
@@ -127,7 +146,7 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
   lane_batch(ex, 0, P.bdim * (2 * P.m + 1), [&](int it) {
     return it < P.bdim ? -zv[P.oRho + it] : -zv[P.oMup + (it - P.bdim)];
   }, [&](int it, double v) { out[P.rRisk + it] = v; });
-  const double* boost = C.at(C.L->boost);
+  const gdouble* boost = C.at(C.L->boost);
   const double Qs = P.desc.Qslack[1];
   BMPC_TOC(C.ws, *C.L, PROF_G_LP, t_glp);
   BMPC_TIC(t_gcone);
@@ -141,8 +160,7 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
     const int c0 = c >= 0 ? c : 0;
     const int ndx = t.br_ndx[c0], ndu = t.br_ndu[c0];
     const bool hasch = t.br_child0[c0] >= 0;
-    // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node; the
-    // group's lane 0 folds the risk-variable terms into its partial
+    // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node
     {
       // the root cone (c < 0) holds the root node's slacks only (ndx = br_ndx[0] = 0)
       const int nn = c >= 0 ? P.N : (k >= 0 ? 1 : 0);
@@ -150,20 +168,24 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
       double part = strided_partial<4>(G.gl, G.cg, nn, [&](int j) {
         double a = 0.0;
 #pragma unroll
-        for (int r2 = 0; r2 < NX; ++r2) a += xon * C.qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
+        for (int r2 = 0; r2 < NX; ++r2) a += xon * qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
         for (int cc = 0; cc < P.Nc; ++cc) a += Qs * zv[P.oS + (ndx + j) * P.Nc + cc];
         return a;
       });
+      // risk-variable terms, loaded before the reduction and added after it
+      double tail = 0.0;
       if (k >= 0 && G.gl == 0) {
         if (c >= 0) {
-          double acc = zv[P.oSig + cb] + zv[P.oMup + cb + ci] - zv[P.oMum + cb + ci];
-          if (hasch) acc += zv[P.oRho + c];
-          part += acc;
+          tail = zv[P.oSig + cb] + zv[P.oMup + cb + ci] - zv[P.oMum + cb + ci];
         } else {
-          part += -zv[P.oJ] + zv[P.oRho + 0];
+          tail = -zv[P.oJ] + zv[P.oRho + 0];
         }
       }
-      const double f = ex.gsum(part, G.cg) * ebst;
+      const double rho_c = (k >= 0 && G.gl == 0 && c >= 0 && hasch) ? zv[P.oRho + c] : 0.0;
+      double acc = ex.gsum(part, G.cg);
+      acc += tail;
+      if (c >= 0 && hasch) acc += rho_c;
+      const double f = acc * ebst;
       if (k >= 0 && G.gl == 0) {
         out[off] = f;
         out[off + q - 1] = -f;
@@ -195,13 +217,16 @@ BMPC_FN void apply_G(const X ex, const Ctx& C, const double* zv, double* out) {
 
 // out(nv) = G' r
 template <class X, int NX, int NU>
-BMPC_FN void apply_GT(const X ex, const Ctx& C, const double* r, double* out) {
-  const Plan& P = *C.P;
+BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out) {
+  const Ctx C = Cin.uniform();
+  double qx[NX];
+  ctx_qx<NX>(C, qx);
+  CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYGT);
-  const Topo& t = P.t;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  const double* boost = C.at(C.L->boost);
-  const double* dh = C.at(C.L->dh);
+  const gdouble* boost = C.at(C.L->boost);
+  const gdouble* dh = C.at(C.L->dh);
   const double Qs = P.desc.Qslack[1];
   // state nodes: x and S parts (all loads of a node first, stores after)
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -219,7 +244,7 @@ BMPC_FN void apply_GT(const X ex, const Ctx& C, const double* r, double* out) {
         double v = 0.0;
 #pragma unroll
         for (int rr = 0; rr < NX; ++rr) v += -2.0 * P.W1[rr * NX + s2] * r[off + 1 + j * NX + rr];
-        cx[s2] = v - 2.0 * C.qx[s2] * f;
+        cx[s2] = v - 2.0 * qx[s2] * f;
       }
       fS = Qs * f;
     } else if (k == 0) {  // root slack in the root cone
@@ -295,11 +320,11 @@ BMPC_FN void apply_GT(const X ex, const Ctx& C, const double* r, double* out) {
 
 // out(neq) = A zv
 template <class X, int NX, int NU>
-BMPC_HD void apply_A(const X ex, const Ctx& C, const double* zv, double* out) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
-  const double* Ad = C.at(C.L->Ad);
-  const double* Bd = C.at(C.L->Bd);
+BMPC_HD void apply_A(const X ex, const Ctx& C, const gdouble* zv, gdouble* out) {
+  CPlan& P = *C.P;
+  auto& t = P.t;
+  const gdouble* Ad = C.at(C.L->Ad);
+  const gdouble* Bd = C.at(C.L->Bd);
   struct V4 { double v[NX]; };
   lane_batch<2>(ex, 0, P.T, [&](int k) {
     const int su = t.x_srcu[k], sx = t.x_srcx[k];
@@ -325,10 +350,10 @@ BMPC_HD void apply_A(const X ex, const Ctx& C, const double* zv, double* out) {
 #pragma unroll
     for (int r = 0; r < NX; ++r) out[k * NX + r] = o.v[r];
   });
-  const double* p = C.at(C.L->p);
+  const gdouble* p = C.at(C.L->p);
   for (int b = ex.lane; b < P.bdim; b += ex.nlanes) {
     double v = zv[P.oRho + b] + zv[P.oSig + b];
-    for (int i = 0; i < P.m; ++i) v -= p[b * P.m + i] / C.ralpha * zv[P.oMum + b * P.m + i];
+    for (int i = 0; i < P.m; ++i) v -= p[b * P.m + i] / P.desc.ralpha * zv[P.oMum + b * P.m + i];
     out[P.T * NX + b] = v;
   }
   ex.sync();
@@ -336,11 +361,11 @@ BMPC_HD void apply_A(const X ex, const Ctx& C, const double* zv, double* out) {
 
 // out(nv) = A' y
 template <class X, int NX, int NU>
-BMPC_HD void apply_AT(const X ex, const Ctx& C, const double* y, double* out) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
-  const double* Ad = C.at(C.L->Ad);
-  const double* Bd = C.at(C.L->Bd);
+BMPC_HD void apply_AT(const X ex, const Ctx& C, const gdouble* y, gdouble* out) {
+  CPlan& P = *C.P;
+  auto& t = P.t;
+  const gdouble* Ad = C.at(C.L->Ad);
+  const gdouble* Bd = C.at(C.L->Bd);
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     double ax[NX], au[NU];
 #pragma unroll
@@ -378,7 +403,7 @@ BMPC_HD void apply_AT(const X ex, const Ctx& C, const double* y, double* out) {
     for (int r = 0; r < NX; ++r) out[P.oX + k * NX + r] = ax[r];
   }
   lane_batch(ex, P.oS, P.oJ, [&](int) { return 0.0; }, [&](int i, double v) { out[i] = v; });
-  const double* p = C.at(C.L->p);
+  const gdouble* p = C.at(C.L->p);
   for (int i = ex.lane; i < P.ng; i += ex.nlanes) {
     const int gi = i == P.ng - 1 ? P.oJ : P.oRho + i;
     double v = 0.0;
@@ -386,7 +411,7 @@ BMPC_HD void apply_AT(const X ex, const Ctx& C, const double* y, double* out) {
     else if (gi < P.oMup) v = y[P.T * NX + (gi - P.oSig)];
     else if (gi >= P.oMum && gi < P.oS) {
       const int j = gi - P.oMum, b = j / P.m, ii = j % P.m;
-      v = -p[b * P.m + ii] / C.ralpha * y[P.T * NX + b];
+      v = -p[b * P.m + ii] / P.desc.ralpha * y[P.T * NX + b];
     }
     out[gi] = v;
   }
@@ -395,11 +420,11 @@ BMPC_HD void apply_AT(const X ex, const Ctx& C, const double* y, double* out) {
 
 // h (rows) and b (eq) of this solve
 template <class X, int NX, int NU>
-BMPC_HD void build_hb(const X ex, const Ctx& C, double* h, double* bv) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
+BMPC_HD void build_hb(const X ex, const Ctx& C, gdouble* h, gdouble* bv) {
+  CPlan& P = *C.P;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  const double* h0 = C.at(C.L->h0);
+  const gdouble* h0 = C.at(C.L->h0);
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
     const int k = it / Nc, c = it % Nc;
     double v = 0.0;
@@ -409,7 +434,7 @@ BMPC_HD void build_hb(const X ex, const Ctx& C, double* h, double* bv) {
   }
   for (int it = ex.lane; it < P.U * P.nFu; it += ex.nlanes) h[P.rFu + it] = P.desc.bu[it % P.nFu];
   for (int it = ex.lane; it < P.bdim * (2 * P.m + 1); it += ex.nlanes) h[P.rRisk + it] = 0.0;
-  const double* boost = C.at(C.L->boost);
+  const gdouble* boost = C.at(C.L->boost);
   for (int k = 0; k < P.ncones; ++k) {
     const int off = t.cone_off[k], q = t.cone_q[k];
     for (int i = ex.lane; i < q; i += ex.nlanes) h[off + i] = 0.0;
@@ -417,14 +442,14 @@ BMPC_HD void build_hb(const X ex, const Ctx& C, double* h, double* bv) {
   ex.sync();
   for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
     const int off = t.cone_off[k], q = t.cone_q[k];
-    const double a = t.cone_c[k] >= 0 ? C.jcons * P.N : 0.0;
+    const double a = t.cone_c[k] >= 0 ? C.ws[C.L->misc + MISC_JCONS] * P.N : 0.0;
     const double h0v = 1.0 - a, hlv = 1.0 + a;
     const double ch = cosh(boost[k]), sh = sinh(boost[k]);
     h[off] = ch * h0v + sh * hlv;
     h[off + q - 1] = sh * h0v + ch * hlv;
   }
-  const double* Cd = C.at(C.L->Cd);
-  const double* xbar = C.at(C.L->xbar);
+  const gdouble* Cd = C.at(C.L->Cd);
+  const gdouble* xbar = C.at(C.L->xbar);
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int su = t.x_srcu[k];
     for (int r = 0; r < NX; ++r) bv[k * NX + r] = su >= 0 ? Cd[su * NX + r] : xbar[r];
@@ -438,14 +463,15 @@ BMPC_HD void build_hb(const X ex, const Ctx& C, double* h, double* bv) {
 // ------------------------------------------------------------------------------------
 // returns false when an iterate left its cone
 template <class X>
-BMPC_FN bool compute_scaling(const X ex, const Ctx& C, const double* s, const double* z) {
+BMPC_FN bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s, const gdouble* z) {
+  const Ctx C = Cin.uniform();
   BMPC_PROF(C.ws, *C.L, PROF_SCALING);
-  const Plan& P = *C.P;
-  double* dl = C.at(C.L->dl);
-  double* lam = C.at(C.L->lam);
-  double* eta = C.at(C.L->eta);
-  double* wb = C.at(C.L->wbar);
-  double* vn = C.at(C.L->vnt);
+  CPlan& P = *C.P;
+  gdouble* dl = C.at(C.L->dl);
+  gdouble* lam = C.at(C.L->lam);
+  gdouble* eta = C.at(C.L->eta);
+  gdouble* wb = C.at(C.L->wbar);
+  gdouble* vn = C.at(C.L->vnt);
   struct DL { double d, l; };
   double bad = strided_partial<8, 1>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
     return (s[i] > 0.0 && z[i] > 0.0) ? 0.0 : 1.0;
@@ -487,10 +513,10 @@ BMPC_FN bool compute_scaling(const X ex, const Ctx& C, const double* s, const do
 // identity scaling for the initial point
 template <class X>
 BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
-  const Plan& P = *C.P;
-  double* dl = C.at(C.L->dl);
-  double* wb = C.at(C.L->wbar);
-  double* vn = C.at(C.L->vnt);
+  CPlan& P = *C.P;
+  gdouble* dl = C.at(C.L->dl);
+  gdouble* wb = C.at(C.L->wbar);
+  gdouble* vn = C.at(C.L->vnt);
   lane_batch(ex, 0, P.nlp, [&](int) { return 1.0; }, [&](int i, double v) { dl[i] = v; });
   const int c0 = P.nlp;
   lane_batch(ex, c0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { wb[i] = v; vn[i] = v; });
@@ -505,17 +531,17 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
 
 // mode 0: W v, 1: W^-1 v, 2: W^2 v, 3: W^-2 v   (W symmetric NT scaling)
 template <class X>
-BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const double* in, double* out) {
-  const Plan& P = *C.P;
+BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out) {
+  CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
-  const double* dl = C.at(C.L->dl);
+  const gdouble* dl = C.at(C.L->dl);
   lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
     return mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
   }, [&](int i, double v) { out[i] = v; });
-  const double* eta = C.at(C.L->eta);
+  const gdouble* eta = C.at(C.L->eta);
   // W = e (2 v v' - J); W^-1 = (2 Jv Jv' - J)/e; W^2 = e^2 (2 wb wb' - J); W^-2 = (2 Jwb Jwb' - J)/e^2
-  const double* a = C.at((mode == 0 || mode == 1) ? C.L->vnt : C.L->wbar);
+  const gdouble* a = C.at((mode == 0 || mode == 1) ? C.L->vnt : C.L->wbar);
   const bool jconj = (mode == 1 || mode == 3);
   constexpr int UC = 8;   // cone rows per lane held in registers between the two passes
   BMPC_CONE_ROUNDS(ex, P, G) {
@@ -556,8 +582,8 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const double* in, doubl
 
 // Jordan product out = u o v
 template <class X>
-BMPC_HD void jprod(const X ex, const Ctx& C, const double* u, const double* v, double* out) {
-  const Plan& P = *C.P;
+BMPC_HD void jprod(const X ex, const Ctx& C, const gdouble* u, const gdouble* v, gdouble* out) {
+  CPlan& P = *C.P;
   lane_batch(ex, 0, P.nlp, [&](int i) { return u[i] * v[i]; }, [&](int i, double r) { out[i] = r; });
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
@@ -571,8 +597,8 @@ BMPC_HD void jprod(const X ex, const Ctx& C, const double* u, const double* v, d
 
 // out = lam \ v  (lam o out = v)
 template <class X>
-BMPC_HD void jdiv(const X ex, const Ctx& C, const double* lam, const double* v, double* out) {
-  const Plan& P = *C.P;
+BMPC_HD void jdiv(const X ex, const Ctx& C, const gdouble* lam, const gdouble* v, gdouble* out) {
+  CPlan& P = *C.P;
   lane_batch(ex, 0, P.nlp, [&](int i) { return v[i] / lam[i]; }, [&](int i, double r) { out[i] = r; });
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
@@ -589,8 +615,9 @@ BMPC_HD void jdiv(const X ex, const Ctx& C, const double* lam, const double* v, 
 
 // largest alpha with lam + alpha d in the cone (ECOS lineSearch for one direction)
 template <class X>
-BMPC_FN double max_step(const X ex, const Ctx& C, const double* lam, const double* d) {
-  const Plan& P = *C.P;
+BMPC_FN double max_step(const X ex, const Ctx Cin, const gdouble* lam, const gdouble* d) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
   double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
     return d[i] < 0.0 ? -lam[i] / d[i] : 1e300;
   });
@@ -617,12 +644,12 @@ BMPC_FN double max_step(const X ex, const Ctx& C, const double* lam, const doubl
 }
 
 // branches of depth dep are contiguous in BFS order: sum_{i<dep} m^i .. + m^dep
-BMPC_HD int branch_count(const Plan& P, int dep) {
+BMPC_HD int branch_count(CPlan& P, int dep) {
   int c = 1;
   for (int i = 0; i < dep; ++i) c *= P.m;
   return c;
 }
-BMPC_HD int branch_start(const Plan& P, int dep) {
+BMPC_HD int branch_start(CPlan& P, int dep) {
   int s = 0, c = 1;
   for (int i = 0; i < dep; ++i) s += c, c *= P.m;
   return s;
@@ -631,8 +658,8 @@ BMPC_HD int branch_start(const Plan& P, int dep) {
 // one Riccati step at a node with input: P = hx + A'Pb A - Qux' Quu^-1 Qux,
 // Quu = hu + B'Pb B (Cholesky stored), K = -Quu^-1 Qux (stored).  Pout receives P.
 template <int NX, int NU>
-BMPC_HD bool riccati_step(const double* hx, const double* hu, const double* Ap, const double* Bp,
-                          const double (&Pb)[NX][NX], double (&Pk)[NX][NX], double* Luu_out, double* K_out) {
+BMPC_HD bool riccati_step(const gdouble* hx, const gdouble* hu, const gdouble* Ap, const gdouble* Bp,
+                          const double (&Pb)[NX][NX], double (&Pk)[NX][NX], gdouble* Luu_out, gdouble* K_out) {
   double A[NX][NX], B[NX][NU], M[NX][NX];
   mat_load(Pk, hx);
   mat_load(A, Ap);
@@ -717,17 +744,20 @@ BMPC_HD bool riccati_step(const double* hx, const double* hu, const double* Ap, 
 // KKT factorisation
 // ------------------------------------------------------------------------------------
 template <class X, int NX, int NU>
-BMPC_FN bool kkt_factor(const X ex, const Ctx& C) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
+BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
+  const Ctx C = Cin.uniform();
+  double qx[NX];
+  ctx_qx<NX>(C, qx);
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_FACTOR);
-  const Topo& t = P.t;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  double* ws = C.ws;
-  const double* dl = ws + L.dl;
-  const double* eta = ws + L.eta;
-  const double* wb = ws + L.wbar;
-  const double* boost = ws + L.boost;
+  gdouble* ws = C.ws;
+  const gdouble* dl = ws + L.dl;
+  const gdouble* eta = ws + L.eta;
+  const gdouble* wb = ws + L.wbar;
+  const gdouble* boost = ws + L.boost;
   const double Qs = P.desc.Qslack[1];
   // ---- node Hessian blocks (LP rows with slack elimination + cone F2'F2/eta^2) ----------
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -776,23 +806,23 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx& C) {
   }
   // ---- rank-1 cone vectors g_k = G_k'(J wbar) (boosted rows) ----------------------------
   for (int k = 0; k < P.ncones; ++k) {
-    double* g = ws + L.gk + (size_t)k * P.nv;
+    gdouble* g = ws + L.gk + (size_t)k * P.nv;
     for (int i = ex.lane; i < P.nv; i += ex.nlanes) g[i] = 0.0;
   }
   ex.sync();
   for (int k = 0; k < P.ncones; ++k) {
-    double* g = ws + L.gk + (size_t)k * P.nv;
+    gdouble* g = ws + L.gk + (size_t)k * P.nv;
     const int off = t.cone_off[k], q = t.cone_q[k], c = t.cone_c[k];
     const double kap = (wb[off] + wb[off + q - 1]) * exp(-boost[k]);
     if (c >= 0) {
       for (int it = ex.lane; it < P.N; it += ex.nlanes) {
         const int xk = t.br_ndx[c] + it, uk = t.br_ndu[c] + it;
-        const double* wx = wb + off + 1 + it * NX;
-        const double* wu = wb + off + 1 + P.N * NX + it * NU;
+        const gdouble* wx = wb + off + 1 + it * NX;
+        const gdouble* wu = wb + off + 1 + P.N * NX + it * NU;
         for (int s = 0; s < NX; ++s) {
           double v = 0.0;
           for (int r = 0; r < NX; ++r) v += P.W1[r * NX + s] * wx[r];
-          g[P.oX + xk * NX + s] = kap * (-2.0 * C.qx[s]) + 2.0 * v;
+          g[P.oX + xk * NX + s] = kap * (-2.0 * qx[s]) + 2.0 * v;
         }
         for (int s = 0; s < NU; ++s) {
           double v = 0.0;
@@ -823,8 +853,8 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx& C) {
   // ---- tree Riccati factorisation (leaves -> root), one lane per branch --------------------
   // The cost-to-go P runs backward along each branch in registers; only at a branch end are
   // the children's first-node P read back (written by the previous depth phase).
-  const double* Ad = ws + L.Ad;
-  const double* Bd = ws + L.Bd;
+  const gdouble* Ad = ws + L.Ad;
+  const gdouble* Bd = ws + L.Bd;
   double bad = 0.0;
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
@@ -846,7 +876,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx& C) {
           mat_zero(Pb);
           const int c0 = t.br_child0[b];
           for (int i = 0; i < P.m; ++i) {
-            const double* Pc = ws + L.P + t.br_ndx[c0 + i] * NX * NX;
+            const gdouble* Pc = ws + L.P + t.br_ndx[c0 + i] * NX * NX;
 #pragma unroll
             for (int r = 0; r < NX; ++r)
 #pragma unroll
@@ -885,29 +915,30 @@ BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[N
 // the affine term l / the state x in registers along the branch -- only the Riccati data
 // is loaded per node; (3) lane-parallel post-pass: multipliers nu and slack recovery.
 template <class X, int NX, int NU>
-BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r,
-                        const double* const* e, double* const* out, double* const* nu) {
+BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const* r,
+                        const gdouble* const* e, gdouble* const* out, gdouble* const* nu) {
+  const Ctx C = Cin.uniform();
   constexpr int W = X::kTaskLanes;
   constexpr int RX = (NX + W - 1) / W;
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_TREESOLVE);
   BMPC_COUNT(C.ws, L, PROF_NTREE);
-  const Topo& t = P.t;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  double* ws = C.ws;
-  double* lv_ = ws + L.lvec;   // [nr][T][NX]
-  double* q0_ = ws + L.qx0;    // [nr][T][NX]
-  double* kf_ = ws + L.kff;    // [nr][U][NU]
+  gdouble* ws = C.ws;
+  gdouble* lv_ = ws + L.lvec;   // [nr][T][NX]
+  gdouble* q0_ = ws + L.qx0;    // [nr][T][NX]
+  gdouble* kf_ = ws + L.kff;    // [nr][U][NU]
   const size_t lstr = (size_t)P.T * NX, kstr = (size_t)P.U * NU;
-  const double* dh = ws + L.dh;
-  const double* sdv = ws + L.sd;
+  const gdouble* dh = ws + L.dh;
+  const gdouble* sdv = ws + L.sd;
   const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
 
   // ---- (1) pre-pass: qx0 = -r_x - sum_c f_c df r_S / sd (non-terminal nodes) -------------
   for (int ri = 0; ri < nr; ++ri) {
-    const double* rr = r[ri];
-    double* q0 = q0_ + ri * lstr;
+    const gdouble* rr = r[ri];
+    gdouble* q0 = q0_ + ri * lstr;
     lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
       const int k = it / NX, j = it % NX;
       double v = -rr[P.oX + it];
@@ -930,11 +961,11 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
       const int task = rd * ngrp + grp;
       if (task >= ntask) continue;       // whole group idle together
       const int b = b0 + task / nr, ri = task % nr;
-      const double* rr = r[ri];
-      const double* ee = e[ri];
-      double* lvec = lv_ + ri * lstr;
-      const double* q0 = q0_ + ri * lstr;
-      double* kf = kf_ + ri * kstr;
+      const gdouble* rr = r[ri];
+      const gdouble* ee = e[ri];
+      gdouble* lvec = lv_ + ri * lstr;
+      const gdouble* q0 = q0_ + ri * lstr;
+      gdouble* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
       const int c0 = t.br_child0[b];
@@ -1049,9 +1080,9 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
       const int task = rd * ngrp + grp;
       if (task >= ntask) continue;
       const int b = b0 + task / nr, ri = task % nr;
-      double* o = out[ri];
-      const double* ee = e[ri];
-      const double* kf = kf_ + ri * kstr;
+      gdouble* o = out[ri];
+      const gdouble* ee = e[ri];
+      const gdouble* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
       const int c0 = t.br_child0[b];
@@ -1124,11 +1155,11 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
 
   // ---- (3) post-pass: nu_k = -(l_k + P_k x_k), slack recovery --------------------------------
   for (int ri = 0; ri < nr; ++ri) {
-    double* o = out[ri];
-    const double* rr = r[ri];
-    const double* lvec = lv_ + ri * lstr;
+    gdouble* o = out[ri];
+    const gdouble* rr = r[ri];
+    const gdouble* lvec = lv_ + ri * lstr;
     if (nu[ri]) {
-      double* nn = nu[ri];
+      gdouble* nn = nu[ri];
       lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
         double v = lvec[it];
@@ -1151,7 +1182,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx& C, int nr, const double* const* r
 
 // dense LU with partial pivoting of the coupling system (row-major n x n, in LDS)
 template <class X>
-BMPC_FN bool small_lu(const X ex, double* M, double* piv, int n) {
+BMPC_FN bool small_lu(const X ex, ldouble* M, ldouble* piv, int n) {
   for (int k = 0; k < n; ++k) {
     double best = -1.0, bi = 1e300;
     for (int i = k + ex.lane; i < n; i += ex.nlanes) {
@@ -1183,7 +1214,7 @@ BMPC_FN bool small_lu(const X ex, double* M, double* piv, int n) {
 
 // solve with the LU above; b in LDS, column-oriented substitution (one step per row)
 template <class X>
-BMPC_HD void small_lu_solve(const X ex, const double* M, const double* piv, double* b, int n) {
+BMPC_HD void small_lu_solve(const X ex, const ldouble* M, const ldouble* piv, ldouble* b, int n) {
   if (ex.lane == 0)
     for (int k = 0; k < n; ++k) {
       const int p = (int)piv[k];
@@ -1209,20 +1240,21 @@ BMPC_HD void small_lu_solve(const X ex, const double* M, const double* piv, doub
 }
 
 // global variable index -> position in the primal vector
-BMPC_HD int gvar(const Plan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
+BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
 
 // Woodbury columns, coupling matrix and its LU; returns false on breakdown
 template <class X, int NX, int NU>
-BMPC_FN bool kkt_coupling(const X ex, const Ctx& C) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
+BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_COUPLING);
-  double* ws = C.ws;
+  gdouble* ws = C.ws;
   const int nc = P.ncones;
-  const double* rr[32];
-  const double* ee[32];
-  double* oo[32];
-  double* nn[32];
+  const gdouble* rr[32];
+  const gdouble* ee[32];
+  gdouble* oo[32];
+  gdouble* nn[32];
   for (int k = 0; k < nc; ++k) {
     rr[k] = ws + L.gk + (size_t)k * P.nv;
     ee[k] = ws + L.zeros;
@@ -1231,18 +1263,18 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx& C) {
   }
   tree_solve<X, NX, NU>(ex, C, nc, rr, ee, oo, nn);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
-  double* M = ex.lds + P.lds_M;
-  const double* eta = ws + L.eta;
-  const double* dl = ws + L.dl;
-  const double* p = ws + L.p;
+  ldouble* M = ex.lds + P.lds_M;
+  const gdouble* eta = ws + L.eta;
+  const gdouble* dl = ws + L.dl;
+  const gdouble* p = ws + L.p;
   const int ntree = P.oRho;    // x and u parts are [0, oRho); S part [oS, oJ)
   for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
   ex.sync();
   // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables
   for (int it = 0; it < nc * nc; ++it) {
     const int k = it / nc, j = it % nc;
-    const double* g = ws + L.gk + (size_t)k * P.nv;
-    const double* col = ws + L.colk + (size_t)j * P.nv;
+    const gdouble* g = ws + L.gk + (size_t)k * P.nv;
+    const gdouble* col = ws + L.colk + (size_t)j * P.nv;
     double s = lane_partial(ex, 0, ntree, [&](int i) { return g[i] * col[i]; }) +
                lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * col[i]; });
     s = ex.sum(s);
@@ -1270,7 +1302,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx& C) {
     M[(nb + b) * ns + row] = 1.0;
     for (int i = 0; i < P.m; ++i) {
       const int gi = 2 * nb + nb * P.m + b * P.m + i;
-      const double a = -p[b * P.m + i] / C.ralpha;
+      const double a = -p[b * P.m + i] / P.desc.ralpha;
       M[row * ns + gi] = a;
       M[gi * ns + row] = a;
     }
@@ -1291,29 +1323,30 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx& C) {
 //   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
 template <class X, int NX, int NU>
-BMPC_FN void kkt_solve_once(const X ex, const Ctx& C, const double* r1, const double* r2,
-                            const double* r3h, double* dx, double* dy, double* dzh) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  double* ws = C.ws;
-  double* tr = ws + L.k_r0;
-  double* tz = ws + L.k_nv0;
+BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
+                            const gdouble* r3h, gdouble* dx, gdouble* dy, gdouble* dzh) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* tr = ws + L.k_r0;
+  gdouble* tz = ws + L.k_nv0;
   apply_W(ex, C, 1, r3h, tr);                     // W^-1 r3h
   apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-1 r3h
   lane_batch<16>(ex, 0, P.nv, [&](int i) { return tz[i] + r1[i]; }, [&](int i, double v) { tz[i] = v; });
   ex.sync();
   {
-    const double* rr[1] = {tz};
-    const double* ee[1] = {r2};
-    double* oo[1] = {dx};
-    double* nn[1] = {dy};
+    const gdouble* rr[1] = {tz};
+    const gdouble* ee[1] = {r2};
+    gdouble* oo[1] = {dx};
+    gdouble* nn[1] = {dy};
     tree_solve<X, NX, NU>(ex, C, 1, rr, ee, oo, nn);
   }
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
-  double* b = ex.lds + P.lds_rhs;
-  const double* eta = ws + L.eta;
+  ldouble* b = ex.lds + P.lds_rhs;
+  const gdouble* eta = ws + L.eta;
   for (int k = 0; k < nc; ++k) {
-    const double* g = ws + L.gk + (size_t)k * P.nv;
+    const gdouble* g = ws + L.gk + (size_t)k * P.nv;
     const double sk = ex.sum(lane_partial(ex, 0, P.oRho, [&](int i) { return g[i] * dx[i]; }) +
                              lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * dx[i]; }));
     if (ex.lane == 0) b[ng + nb + k] = 2.0 / (eta[k] * eta[k]) * sk;
@@ -1321,9 +1354,9 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx& C, const double* r1, const do
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
   small_lu_solve(ex, ex.lds + P.lds_M, ex.lds + P.lds_piv, b, ns);
-  const double* bc = b + ng + nb;
-  const double* colk = ws + L.colk;
-  const double* colnu = ws + L.colnu;
+  const ldouble* bc = b + ng + nb;
+  const gdouble* colk = ws + L.colk;
+  const gdouble* colnu = ws + L.colnu;
   auto woodbury_x = [&](int i) {
     double v = dx[i];
     for (int k = 0; k < nc; ++k) v -= bc[k] * colk[(size_t)k * P.nv + i];
@@ -1353,20 +1386,21 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx& C, const double* r1, const do
 // iterative refinement on the scaled residual (well conditioned, unlike the W^2 form whose
 // residual is dominated by the rounding of W^2 dz near the boundary).
 template <class X, int NX, int NU>
-BMPC_FN void kkt_solve(const X ex, const Ctx& C, const double* r1, const double* r2,
-                       const double* r3, double* dx, double* dy, double* dz) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
+BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
+                       const gdouble* r3, gdouble* dx, gdouble* dy, gdouble* dz) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_KKT);
-  double* ws = C.ws;
-  double* e1 = ws + L.k_e1;
-  double* e2 = ws + L.k_e2;
-  double* e3 = ws + L.k_e3;
-  double* r3h = ws + L.k_t3;
-  double* cx = ws + L.k_cx;
-  double* cy = ws + L.k_cy;
-  double* cz = ws + L.k_cz;
-  double* tv = ws + L.k_nv1;
+  gdouble* ws = C.ws;
+  gdouble* e1 = ws + L.k_e1;
+  gdouble* e2 = ws + L.k_e2;
+  gdouble* e3 = ws + L.k_e3;
+  gdouble* r3h = ws + L.k_t3;
+  gdouble* cx = ws + L.k_cx;
+  gdouble* cy = ws + L.k_cy;
+  gdouble* cz = ws + L.k_cz;
+  gdouble* tv = ws + L.k_nv1;
   apply_W(ex, C, 1, r3, r3h);
   BMPC_COUNT(ws, L, PROF_NSOLVE);
   kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz);   // dz holds dzh until the end
@@ -1411,8 +1445,8 @@ BMPC_FN void kkt_solve(const X ex, const Ctx& C, const double* r1, const double*
 
 // ECOS bring2cone: s = r + (1 + alpha) e
 template <class X>
-BMPC_HD void bring2cone(const X ex, const Ctx& C, const double* r, double* s) {
-  const Plan& P = *C.P;
+BMPC_HD void bring2cone(const X ex, const Ctx& C, const gdouble* r, gdouble* s) {
+  CPlan& P = *C.P;
   double alpha = -0.99;
   const double mn = -ex.min(strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) { return r[i]; }));
   if (P.nlp > 0 && mn >= 0.0 && mn > alpha) alpha = mn;
@@ -1435,7 +1469,7 @@ BMPC_HD void bring2cone(const X ex, const Ctx& C, const double* r, double* s) {
 }
 
 template <class X>
-BMPC_HD double vdot(const X ex, const double* a, const double* b, int n) {
+BMPC_HD double vdot(const X ex, const gdouble* a, const gdouble* b, int n) {
   return lane_sum(ex, 0, n, [&](int i) { return a[i] * b[i]; });
 }
 
@@ -1450,33 +1484,33 @@ struct IpmResult {
 // ------------------------------------------------------------------------------------
 template <class X, int NX, int NU>
 BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  double* ws = C.ws;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
   const int nv = P.nv, neq = P.neq, nr = P.nrows;
-  double* x = ws + L.x;
-  double* y = ws + L.y;
-  double* z = ws + L.z;
-  double* s = ws + L.s;
-  double* lam = ws + L.lam;
-  double* x1 = ws + L.x1;
-  double* y1 = ws + L.y1;
-  double* z1 = ws + L.z1;
-  double* x2 = ws + L.x2;
-  double* y2 = ws + L.y2;
-  double* z2 = ws + L.z2;
-  double* dz = ws + L.dz;
-  double* ds = ws + L.ds;
-  double* rx = ws + L.rx;
-  double* ry = ws + L.ry;
-  double* rz = ws + L.rz;
-  double* hv = ws + L.hvec;
-  double* bv = ws + L.bvec;
-  double* tA = ws + L.ta;
-  double* ya = ws + L.ya;
-  double* ra = ws + L.ra;
-  double* rb = ws + L.rb;
-  double* rc = ws + L.rc;
+  gdouble* x = ws + L.x;
+  gdouble* y = ws + L.y;
+  gdouble* z = ws + L.z;
+  gdouble* s = ws + L.s;
+  gdouble* lam = ws + L.lam;
+  gdouble* x1 = ws + L.x1;
+  gdouble* y1 = ws + L.y1;
+  gdouble* z1 = ws + L.z1;
+  gdouble* x2 = ws + L.x2;
+  gdouble* y2 = ws + L.y2;
+  gdouble* z2 = ws + L.z2;
+  gdouble* dz = ws + L.dz;
+  gdouble* ds = ws + L.ds;
+  gdouble* rx = ws + L.rx;
+  gdouble* ry = ws + L.ry;
+  gdouble* rz = ws + L.rz;
+  gdouble* hv = ws + L.hvec;
+  gdouble* bv = ws + L.bvec;
+  gdouble* tA = ws + L.ta;
+  gdouble* ya = ws + L.ya;
+  gdouble* ra = ws + L.ra;
+  gdouble* rb = ws + L.rb;
+  gdouble* rc = ws + L.rc;
   const double feastol = P.desc.feastol, abstol = P.desc.abstol, reltol = P.desc.reltol;
   const double deg = (double)(P.nlp + P.ncones);
   IpmResult res{EXIT_MAXIT, 0, 0.0};
@@ -1517,7 +1551,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     {   // probe: latency of one dependent global load under the kernel's own load
       BMPC_TIC(t_lat);
-      const double probe = *(volatile const double*)(ws + L.bestx + ex.lane);
+      const double probe = *(volatile const gdouble*)(ws + L.bestx + ex.lane);
       if (probe == 1.2345e300) ws[L.prof + PROF_STEP] += 0.0;
       BMPC_TOC(ws, L, PROF_STEP, t_lat);
     }

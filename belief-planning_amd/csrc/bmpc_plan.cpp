@@ -84,13 +84,13 @@ void weight_root(const double* M, int n, double* W) {
 }  // namespace
 
 void HostPlan::point_tables(const int32_t* base) {
-  const int32_t** ptrs[] = {&plan.t.br_depth, &plan.t.br_len, &plan.t.br_ndx, &plan.t.br_ndu,
+  gint** ptrs[] = {&plan.t.br_depth, &plan.t.br_len, &plan.t.br_ndx, &plan.t.br_ndu,
                             &plan.t.br_child0, &plan.t.x_u, &plan.t.x_srcu, &plan.t.x_srcx,
                             &plan.t.x_cone, &plan.t.x_conepos, &plan.t.x_branch, &plan.t.succ_off,
                             &plan.t.succ, &plan.t.lvl_off, &plan.t.lvl_nodes, &plan.t.u_x,
                             &plan.t.u_cone, &plan.t.cone_b, &plan.t.cone_i, &plan.t.cone_c,
                             &plan.t.cone_q, &plan.t.cone_off};
-  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) *ptrs[i] = base + blob_off[i];
+  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) *ptrs[i] = (gint*)(base + blob_off[i]);
 }
 
 std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {

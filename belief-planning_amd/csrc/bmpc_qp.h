@@ -17,28 +17,30 @@
 namespace bmpc {
 
 struct QpCtx {
-  const Plan* P;
-  const Layout* L;
-  double* ws;
+  CPlan* P;
+  CLayout* L;
+  gdouble* ws;
+  BMPC_HD QpCtx uniform() const { return QpCtx{uniform_ptr(P), uniform_ptr(L), uniform_ptr(ws)}; }
 };
 
 // u node whose input created x node k's state (the rate-cost predecessor of x_u[k]); -1 root
-BMPC_HD int qp_pred_u(const Plan& P, int u) { return P.t.x_srcu[P.t.u_x[u]]; }
+BMPC_HD int qp_pred_u(CPlan& P, int u) { return P.t.x_srcu[P.t.u_x[u]]; }
 
 // ---- cost, rhs (buildCost / buildIneqConstr / buildEqConstr of the current tree) ----------
 template <class X, class M>
-BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
+BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
+  const QpCtx C = Cin.uniform();
   constexpr int NX = M::NX, NU = M::NU;
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
-  double* ws = C.ws;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
+  gdouble* ws = C.ws;
   const int Nc = P.Nc;
-  const double* w = ws + L.w;
-  const double* xbar = ws + L.xbar;
-  const double* xref = ws + L.xref;
-  const double* Q = P.desc.Q;
-  const double* Qf = P.desc.Qf;
+  const gdouble* w = ws + L.w;
+  const gdouble* xbar = ws + L.xbar;
+  const gdouble* xref = ws + L.xref;
+  const auto Q = P.desc.Q;
+  const auto Qf = P.desc.Qf;
   double xq[NX], xqf[NX];
   for (int c = 0; c < NX; ++c) {
     double a = 0.0, b = 0.0;
@@ -46,7 +48,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     xq[c] = a;
     xqf[c] = b;
   }
-  double* q = ws + L.qq;
+  gdouble* q = ws + L.qq;
   // BranchMPCProx: dQ = 3Q (:270); BranchMPC: dQ = 0.5Q, leaf's last node tracks xRef with Qf
   // and the leaf terminal node has no linear term (:1068-1099)
   const bool prox = P.desc.controller == BMPC_CTRL_PROX;
@@ -57,7 +59,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     const double wb = w[b];
     const bool term = t.x_u[k] < 0;
     const bool leaf_last = !term && t.br_child0[b] < 0 && k == t.br_ndx[b] + t.br_len[b] - 1;
-    double* H = ws + L.hx + k * NX * NX;
+    gdouble* H = ws + L.hx + k * NX * NX;
     for (int i = 0; i < NX * NX; ++i) H[i] = 2.0 * wb * (term ? Qf[i] : (dq + 1.0) * Q[i]);   // (dQ + Q) w
     for (int c = 0; c < NX; ++c) {
       double v;
@@ -73,8 +75,8 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     for (int c = 0; c < Nc; ++c) q[P.oS + k * Nc + c] = term ? 0.0 : P.desc.Qslack[1] * wb;
   }
   // input nodes: diagonal blocks (doubled), rate couplings with the predecessor, qu
-  const double* R = P.desc.R;
-  const double* dR = P.desc.dR;
+  const auto R = P.desc.R;
+  const auto dR = P.desc.dR;
   for (int u = ex.lane; u < P.U; u += ex.nlanes) {
     const int k = t.u_x[u], b = t.x_branch[k];
     const int j = k - t.br_ndx[b], len = t.br_len[b];
@@ -96,8 +98,8 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     if (u == 0 && prox)   // Hu[0:d,0:d] += dR (row broadcast), upper triangle read by OSQP
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) D[r][c] += dR[r > c ? r : c];
-    double* Hu = ws + L.hu + u * NU * NU;
-    double* O = ws + L.qo + u * NU * NU;
+    gdouble* Hu = ws + L.hu + u * NU * NU;
+    gdouble* O = ws + L.qo + u * NU * NU;
     const int pu = qp_pred_u(P, u);
     for (int r = 0; r < NU; ++r)
       for (int c = 0; c < NU; ++c) {
@@ -110,7 +112,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
     for (int c = 0; c < NU; ++c) q[P.oU + u * NU + c] = u == 0 ? -2.0 * od : 0.0;
   }
   // rhs of the inequalities: [h0 | bx] per non-terminal node, bu per input, 0 for -S
-  const double* h0 = ws + L.h0;
+  const gdouble* h0 = ws + L.h0;
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
     const int k = it / Nc, c = it % Nc;
     hv[P.rFx + it] = t.x_u[k] < 0 ? 0.0 : (c == 0 ? h0[k] : P.desc.bx[c - 1]);
@@ -118,7 +120,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
   }
   for (int it = ex.lane; it < P.U * P.nFu; it += ex.nlanes) hv[P.rFu + it] = P.desc.bu[it % P.nFu];
   // equality rhs: x0 = x, x_k - A x_src - B u_src = C_src
-  const double* Cd = ws + L.Cd;
+  const gdouble* Cd = ws + L.Cd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int su = t.x_srcu[k];
     for (int r = 0; r < NX; ++r) bv[k * NX + r] = su >= 0 ? Cd[su * NX + r] : xbar[r];
@@ -129,13 +131,14 @@ BMPC_FN void qp_build(const X ex, const QpCtx& C, double* hv, double* bv) {
 // ---- structured operators ------------------------------------------------------------------
 // out = P z  (Hx blocks, Hu diagonal blocks + rate couplings, slack quadratic)
 template <class X, int NX, int NU>
-BMPC_FN void qp_apply_P(const X ex, const QpCtx& C, const double* zv, double* out) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
-  const double* ws = C.ws;
+BMPC_FN void qp_apply_P(const X ex, const QpCtx Cin, const gdouble* zv, gdouble* out) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
+  const gdouble* ws = C.ws;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
-    const double* H = ws + L.hx + k * NX * NX;
+    const gdouble* H = ws + L.hx + k * NX * NX;
     for (int r = 0; r < NX; ++r) {
       double v = 0.0;
       for (int c = 0; c < NX; ++c) v += H[r * NX + c] * zv[P.oX + k * NX + c];
@@ -143,8 +146,8 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx& C, const double* zv, double* ou
     }
   }
   for (int u = ex.lane; u < P.U; u += ex.nlanes) {
-    const double* Hu = ws + L.hu + u * NU * NU;
-    const double* O = ws + L.qo + u * NU * NU;
+    const gdouble* Hu = ws + L.hu + u * NU * NU;
+    const gdouble* O = ws + L.qo + u * NU * NU;
     const int pu = qp_pred_u(P, u);
     double v[NU];
     for (int r = 0; r < NU; ++r) {
@@ -159,7 +162,7 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx& C, const double* zv, double* ou
     for (int e = t.succ_off[k]; e < t.succ_off[k + 1]; ++e) {
       const int su = t.x_u[t.succ[e]];
       if (su < 0) continue;
-      const double* Os = ws + L.qo + su * NU * NU;
+      const gdouble* Os = ws + L.qo + su * NU * NU;
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) v[r] += Os[c * NU + r] * zv[P.oU + su * NU + c];
     }
@@ -172,12 +175,13 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx& C, const double* zv, double* ou
 
 // out(rows) = G z
 template <class X, int NX, int NU>
-BMPC_FN void qp_apply_G(const X ex, const QpCtx& C, const double* zv, double* out) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
+BMPC_FN void qp_apply_G(const X ex, const QpCtx Cin, const gdouble* zv, gdouble* out) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  const double* dh = C.ws + L.dh;
+  const gdouble* dh = C.ws + L.dh;
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     double v = -zv[P.oS + it];
@@ -197,12 +201,13 @@ BMPC_FN void qp_apply_G(const X ex, const QpCtx& C, const double* zv, double* ou
 
 // out(nv) = G' r
 template <class X, int NX, int NU>
-BMPC_FN void qp_apply_GT(const X ex, const QpCtx& C, const double* r, double* out) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
+BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble* out) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  const double* dh = C.ws + L.dh;
+  const gdouble* dh = C.ws + L.dh;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     double ax[NX];
     for (int j = 0; j < NX; ++j) ax[j] = 0.0;
@@ -229,11 +234,12 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx& C, const double* r, double* ou
 
 // E z (dynamics rows) and E' y: the first T*NX rows / x,u parts of the CVaR operators
 template <class X, int NX, int NU>
-BMPC_FN void qp_apply_E(const X ex, const QpCtx& C, const double* zv, double* out) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
-  const double* Ad = C.ws + C.L->Ad;
-  const double* Bd = C.ws + C.L->Bd;
+BMPC_FN void qp_apply_E(const X ex, const QpCtx Cin, const gdouble* zv, gdouble* out) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  auto& t = P.t;
+  const gdouble* Ad = C.ws + C.L->Ad;
+  const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int su = t.x_srcu[k], sx = t.x_srcx[k];
     for (int r = 0; r < NX; ++r) {
@@ -249,11 +255,12 @@ BMPC_FN void qp_apply_E(const X ex, const QpCtx& C, const double* zv, double* ou
 }
 
 template <class X, int NX, int NU>
-BMPC_FN void qp_apply_ET(const X ex, const QpCtx& C, const double* y, double* out) {
-  const Plan& P = *C.P;
-  const Topo& t = P.t;
-  const double* Ad = C.ws + C.L->Ad;
-  const double* Bd = C.ws + C.L->Bd;
+BMPC_FN void qp_apply_ET(const X ex, const QpCtx Cin, const gdouble* y, gdouble* out) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  auto& t = P.t;
+  const gdouble* Ad = C.ws + C.L->Ad;
+  const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     double ax[NX], au[NU];
     for (int r = 0; r < NX; ++r) ax[r] = y[k * NX + r];
@@ -285,15 +292,16 @@ BMPC_FN void qp_apply_ET(const X ex, const QpCtx& C, const double* y, double* ou
 // ---- factorisation: node Hessians of P + G'D^-1G, slack elimination, augmented Riccati -----
 // dinv[i] = z_i / s_i (the inverse of the KKT's D = s/z block)
 template <class X, int NX, int NU>
-BMPC_FN bool qp_factor(const X ex, const QpCtx& C, const double* dinv) {
+BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
+  const QpCtx C = Cin.uniform();
   constexpr int NS = NX + NU;
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  double* ws = C.ws;
+  gdouble* ws = C.ws;
   const double qs2 = 2.0 * P.desc.Qslack[0];
-  const double* dh = ws + L.dh;
+  const gdouble* dh = ws + L.dh;
   // slack pivots sd = qs2 + d_f + d_p (stored with d_f for the solves)
   lane_batch(ex, 0, P.T * Nc, [&](int it) { return dinv[P.rFx + it]; }, [&](int it, double df) {
     ws[L.sd + it * 2] = qs2 + df + dinv[P.rPos + it];
@@ -336,7 +344,7 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx& C, const double* dinv) {
         double Pb[NS][NS];
         mat_zero(Pb);
         for (int e = t.succ_off[k]; e < t.succ_off[k + 1]; ++e) {
-          const double* Pc = ws + L.Pa + t.succ[e] * NS * NS;
+          const gdouble* Pc = ws + L.Pa + t.succ[e] * NS * NS;
           for (int i = 0; i < NS; ++i)
             for (int j = 0; j < NS; ++j) Pb[i][j] += Pc[i * NS + j];
         }
@@ -423,16 +431,17 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx& C, const double* dinv) {
 
 // Solve [H E'; E 0] [v; nu] = [r; e] with H = P + G'D^-1G (slacks eliminated per node)
 template <class X, int NX, int NU>
-BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const double* e, double* out, double* nu) {
+BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const gdouble* e, gdouble* out, gdouble* nu) {
+  const QpCtx C = Cin.uniform();
   constexpr int NS = NX + NU;
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  const Topo& t = P.t;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  auto& t = P.t;
   const int Nc = P.Nc;
-  double* ws = C.ws;
-  const double* dh = ws + L.dh;
-  double* la = ws + L.la;
-  double* kf = ws + L.kff;
+  gdouble* ws = C.ws;
+  const gdouble* dh = ws + L.dh;
+  gdouble* la = ws + L.la;
+  gdouble* kf = ws + L.kff;
   // backward
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
@@ -465,15 +474,15 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
         for (int j = 0; j < NS; ++j) g[j] = 0.0;
         for (int s = t.succ_off[k]; s < t.succ_off[k + 1]; ++s) {
           const int c = t.succ[s];
-          const double* Pc = ws + L.Pa + c * NS * NS;
+          const gdouble* Pc = ws + L.Pa + c * NS * NS;
           for (int i = 0; i < NS; ++i) {
             double v = la[c * NS + i];
             for (int j = 0; j < NX; ++j) v += Pc[i * NS + j] * e[c * NX + j];
             g[i] += v;
           }
         }
-        const double* A = ws + L.Ad + u * NX * NX;
-        const double* B = ws + L.Bd + u * NX * NU;
+        const gdouble* A = ws + L.Ad + u * NX * NX;
+        const gdouble* B = ws + L.Bd + u * NX * NU;
         double qu[NU];
         for (int i = 0; i < NU; ++i) {
           double v = -r[P.oU + u * NU + i] + g[NX + i];
@@ -486,7 +495,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
         chol_solve<NU>(Lu, kv);
         for (int i = 0; i < NU; ++i) kf[u * NU + i] = kv[i];
         // l~ = [qx + A'g_x + Qux' k ; Quv' k], with S = -Quu K  =>  S k = -K' Quu k = K' qu
-        const double* K = ws + L.Ka + u * NU * NS;
+        const gdouble* K = ws + L.Ka + u * NU * NS;
         for (int i = 0; i < NX; ++i) {
           double v = qx[i];
           for (int j = 0; j < NX; ++j) v += A[j * NX + i] * g[j];
@@ -524,7 +533,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
         const int k = ndx + jn;
         const bool term = t.x_u[k] < 0;
         for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = s[j];
-        const double* Pk = ws + L.Pa + k * NS * NS;
+        const gdouble* Pk = ws + L.Pa + k * NS * NS;
         for (int i = 0; i < NX; ++i) {
           double v = la[k * NS + i];
           for (int j = 0; j < NS; ++j) v += Pk[i * NS + j] * s[j];
@@ -539,7 +548,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
         }
         if (term) break;
         const int u = t.x_u[k];
-        const double* K = ws + L.Ka + u * NU * NS;
+        const gdouble* K = ws + L.Ka + u * NU * NS;
         double uk[NU];
         for (int i = 0; i < NU; ++i) {
           double v = kf[u * NU + i];
@@ -547,8 +556,8 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
           uk[i] = v;
           out[P.oU + u * NU + i] = v;
         }
-        const double* A = ws + L.Ad + u * NX * NX;
-        const double* B = ws + L.Bd + u * NX * NU;
+        const gdouble* A = ws + L.Ad + u * NX * NX;
+        const gdouble* B = ws + L.Bd + u * NX * NU;
         double xn[NX];
         for (int i = 0; i < NX; ++i) {
           double v = 0.0;
@@ -575,21 +584,22 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx& C, const double* r, const do
 // KKT solve [P E' G'; E 0 0; G 0 -D] [dx; dy; dz] = [r1; r2; r3], D = s/z, with iterative
 // refinement on the D^-1/2-scaled residual (BMPC_NITREF rounds; oracle: 3 rounds, 1e-15 unscaled)
 template <class X, int NX, int NU>
-BMPC_FN void qp_kkt_solve(const X ex, const QpCtx& C, const double* dinv, const double* r1, const double* r2,
-                          const double* r3, double* dx, double* dy, double* dz) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  double* ws = C.ws;
-  double* tr = ws + L.k_r0;
-  double* tz = ws + L.k_nv0;
-  double* e1 = ws + L.k_e1;
-  double* e2 = ws + L.k_e2;
-  double* e3 = ws + L.k_e3;
-  double* cx = ws + L.k_cx;
-  double* cy = ws + L.k_cy;
-  double* cz = ws + L.k_cz;
-  double* tv = ws + L.k_nv1;
-  auto once = [&](const double* a1, const double* a2, const double* a3, double* ox, double* oy, double* oz) {
+BMPC_FN void qp_kkt_solve(const X ex, const QpCtx Cin, const gdouble* dinv, const gdouble* r1, const gdouble* r2,
+                          const gdouble* r3, gdouble* dx, gdouble* dy, gdouble* dz) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* tr = ws + L.k_r0;
+  gdouble* tz = ws + L.k_nv0;
+  gdouble* e1 = ws + L.k_e1;
+  gdouble* e2 = ws + L.k_e2;
+  gdouble* e3 = ws + L.k_e3;
+  gdouble* cx = ws + L.k_cx;
+  gdouble* cy = ws + L.k_cy;
+  gdouble* cz = ws + L.k_cz;
+  gdouble* tv = ws + L.k_nv1;
+  auto once = [&](const gdouble* a1, const gdouble* a2, const gdouble* a3, gdouble* ox, gdouble* oy, gdouble* oz) {
     // (P + G'D^-1G) ox + E'oy = a1 + G'D^-1 a3 ; E ox = a2 ; oz = D^-1 (G ox - a3)
     lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dinv[i] * a3[i]; }, [&](int i, double v) { tr[i] = v; });
     ex.sync();
@@ -635,29 +645,30 @@ BMPC_FN void qp_kkt_solve(const X ex, const QpCtx& C, const double* dinv, const 
 
 // ---- Mehrotra loop (oracle/qp_ipm.osqp_like_solve) -------------------------------------------
 template <class X, int NX, int NU>
-BMPC_FN IpmResult qp_ipm(const X ex, const QpCtx& C) {
-  const Plan& P = *C.P;
-  const Layout& L = *C.L;
-  double* ws = C.ws;
+BMPC_FN IpmResult qp_ipm(const X ex, const QpCtx Cin) {
+  const QpCtx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
   const int nv = P.nv, neq = P.neq, m = P.nrows;
-  double* x = ws + L.x;
-  double* y = ws + L.y;
-  double* z = ws + L.z;
-  double* s = ws + L.s;
-  double* dinv = ws + L.dl;
-  double* dx = ws + L.x2;
-  double* dy = ws + L.y2;
-  double* dz = ws + L.z2;
-  double* ds = ws + L.ds;
-  double* rd = ws + L.rx;
-  double* re = ws + L.ry;
-  double* rg = ws + L.rz;
-  double* g = ws + L.hvec;
-  double* e = ws + L.bvec;
-  double* q = ws + L.qq;
-  double* t1 = ws + L.ta;
-  double* t2 = ws + L.ya;
-  double* t3 = ws + L.ra;
+  gdouble* x = ws + L.x;
+  gdouble* y = ws + L.y;
+  gdouble* z = ws + L.z;
+  gdouble* s = ws + L.s;
+  gdouble* dinv = ws + L.dl;
+  gdouble* dx = ws + L.x2;
+  gdouble* dy = ws + L.y2;
+  gdouble* dz = ws + L.z2;
+  gdouble* ds = ws + L.ds;
+  gdouble* rd = ws + L.rx;
+  gdouble* re = ws + L.ry;
+  gdouble* rg = ws + L.rz;
+  gdouble* g = ws + L.hvec;
+  gdouble* e = ws + L.bvec;
+  gdouble* q = ws + L.qq;
+  gdouble* t1 = ws + L.ta;
+  gdouble* t2 = ws + L.ya;
+  gdouble* t3 = ws + L.ra;
   const double tol = 1e-10;
   IpmResult res{-2, 0, 0.0};
   // initial point with D = I
@@ -675,13 +686,13 @@ BMPC_FN IpmResult qp_ipm(const X ex, const QpCtx& C) {
   lane_batch<16>(ex, 0, m, [&](int i) { return SZ{s[i] + a0 + 1.0, fmax(fabs(z[i]), 1.0)}; },
                  [&](int i, SZ v) { s[i] = v.s; z[i] = v.z; });
   ex.sync();
-  auto amax_inf = [&](int n, const double* a) {
+  auto amax_inf = [&](int n, const gdouble* a) {
     return ex.max(strided_partial<8, 1>(ex.lane, ex.nlanes, n, [&](int i) { return fabs(a[i]); }));
   };
   const double nq = fmax(1.0, amax_inf(nv, q));
   const double ne = fmax(1.0, amax_inf(neq, e));
   const double ng = fmax(1.0, amax_inf(m, g));
-  auto step_to_boundary = [&](const double* v, const double* dv) {
+  auto step_to_boundary = [&](const gdouble* v, const gdouble* dv) {
     return ex.min(strided_partial<8, 2>(ex.lane, ex.nlanes, m, [&](int i) {
       return dv[i] < 0.0 ? -v[i] / dv[i] : 1e300;
     }));
@@ -749,12 +760,12 @@ BMPC_FN IpmResult qp_ipm(const X ex, const QpCtx& C) {
 template <class X, class M>
 BMPC_HD IpmResult solve_ego_qp(const X& ex, const Plan& P, const Layout& L, EgoView E) {
   constexpr int NX = M::NX, NU = M::NU;
-  double* ws = E.ws;
-  QpCtx C{&P, &L, ws};
+  gdouble* ws = (gdouble*)E.ws;
+  QpCtx C{(CPlan*)&P, (CLayout*)&L, ws};
   qp_build<X, M>(ex, C, ws + L.hvec, ws + L.bvec);
   IpmResult r = qp_ipm<X, NX, NU>(ex, C);
   if (r.exit_flag == 1) {
-    const double* sol = ws + L.sol;
+    const gdouble* sol = ws + L.sol;
     for (int i = ex.lane; i < P.U * NU; i += ex.nlanes) {
       const double v = sol[P.oU + i];
       ws[L.upred + i] = v;

@@ -17,23 +17,19 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
   double* ws = E.ws;
   const bool init = ws[L.misc + MISC_INIT] != 0.0;
   const double* xref = ws + L.xref;
-  Ctx C;
-  C.P = &P;
-  C.L = &L;
-  C.ws = ws;
-  C.ralpha = P.desc.ralpha;
-  for (int c = 0; c < NX; ++c) {
-    double v = 0.0;
-    for (int r = 0; r < NX; ++r) v += xref[r] * P.desc.Q[r * NX + c];
-    C.qx[c] = v;
-  }
-  if (!init) {   // first solve freezes Jcons = xRef Q xRef (MPC_branch.py:1939)
+  if (!init && ex.lane == 0) {   // first solve freezes Jcons = xRef Q xRef (MPC_branch.py:1939)
     double j = 0.0;
-    for (int c = 0; c < NX; ++c) j += C.qx[c] * xref[c];
-    C.jcons = j;
-  } else {
-    C.jcons = ws[L.misc + MISC_JCONS];
+    for (int c = 0; c < NX; ++c) {
+      double v = 0.0;
+      for (int r = 0; r < NX; ++r) v += xref[r] * P.desc.Q[r * NX + c];
+      j += v * xref[c];
+    }
+    ws[L.misc + MISC_JCONS] = j;
   }
+  Ctx C;
+  C.P = (CPlan*)&P;
+  C.L = (CLayout*)&L;
+  C.ws = (gdouble*)ws;
   ex.sync();
   IpmResult r = ipm_solve<X, NX, NU>(ex, C);
   // ---- unpack -----------------------------------------------------------------------------
@@ -52,7 +48,6 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
   ex.sync();
   if (ex.lane == 0) {
     ws[L.misc + MISC_INIT] = 1.0;
-    ws[L.misc + MISC_JCONS] = C.jcons;
     for (int i = 0; i < NU; ++i) ws[L.misc + MISC_OLDU + i] = ws[L.upred + i];
   }
   ex.sync();
