@@ -54,6 +54,23 @@ def main(out):
     summ["pmc"] = agg
     with open(os.path.join(out, "summary.json"), "w") as f:
         json.dump(summ, f, indent=1)
+    # per-launch HBM bytes of the IPM kernel (the figure bench.py reports as roofline.traffic)
+    for k in ("k_ipm", "k_qp"):
+        a = agg.get(k, {})
+        if "FETCH_SIZE" in a and "WRITE_SIZE" in a:
+            fk = a["FETCH_SIZE"]["avg_per_dispatch"]
+            wk = a["WRITE_SIZE"]["avg_per_dispatch"]
+            byt = (2.0 * fk + wk) * 1024.0
+            dur = summ.get("kernel_durations_ns", {}).get(k, {}).get("avg")
+            tj = {"kernel": k, "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes ({out})",
+                  "FETCH_SIZE_kB_per_dispatch": fk, "WRITE_SIZE_kB_per_dispatch": wk,
+                  "correction": "gfx950: FETCH_SIZE counts half of the bytes of wide streaming reads "
+                                "(MI355X_MICROARCH.md, HBM section); doubled here. Our loads are mostly 8 B/lane "
+                                "(uncalibrated width), so the read figure is an upper estimate.",
+                  f"{k}_bytes_per_launch": byt, "avg_dispatch_ns": dur,
+                  "hbm_GBps": byt / dur if dur else None}
+            with open(os.path.join(out, f"{k}_pmc_traffic.json"), "w") as f:
+                json.dump(tj, f, indent=1)
     for d in ("stats", "fetch", "write", "sq", "tcc"):
         shutil.rmtree(os.path.join(out, d), ignore_errors=True)
     print(json.dumps(summ.get("kernel_durations_ns", {}), indent=1))
