@@ -19,6 +19,12 @@
 #ifndef BMPC_NITREF
 #define BMPC_NITREF 1        // refinement rounds per KKT solve (oracle: 3; 1 keeps parity)
 #endif
+#ifndef BMPC_NITREF_INIT
+#define BMPC_NITREF_INIT 0   // refinement rounds of the two initial-point solves (far from the tolerances)
+#endif
+#ifndef BMPC_REFSCORE
+#define BMPC_REFSCORE 1e-3   // refine only when max(pres, dres, relgap) of the iterate < this (1e-4 flips replay exit codes)
+#endif
 #ifndef BMPC_REFTOL
 #define BMPC_REFTOL 1e-14    // refinement stop: scaled residual <= tol * max(1, |rhs|) (oracle: 1e-14)
 #endif
@@ -1387,7 +1393,7 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
 // residual is dominated by the rounding of W^2 dz near the boundary).
 template <class X, int NX, int NU>
 BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
-                       const gdouble* r3, gdouble* dx, gdouble* dy, gdouble* dz) {
+                       const gdouble* r3, gdouble* dx, gdouble* dy, gdouble* dz, int nitref) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
@@ -1404,10 +1410,10 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
   apply_W(ex, C, 1, r3, r3h);
   BMPC_COUNT(ws, L, PROF_NSOLVE);
   kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz);   // dz holds dzh until the end
-  const double sc = ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
+  const double sc = nitref == 0 ? 0.0 : ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
                                      strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
                                 strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
-  for (int itr = 0; itr < BMPC_NITREF; ++itr) {
+  for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     ProfScope _pr(C.ws, L.prof, PROF_REFINE);
 #endif
@@ -1526,7 +1532,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   }
   lane_batch<16>(ex, 0, nv, [&](int i) { return 0.0; }, [&](int i, double v) { tA[i] = v; });
   ex.sync();
-  kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x, y2, z2);
+  kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x, y2, z2, BMPC_NITREF_INIT);
   lane_batch<16>(ex, 0, nr, [&](int i) { return -z2[i]; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
   bring2cone(ex, C, ra, s);
@@ -1534,7 +1540,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   lane_batch(ex, 0, neq, [&](int i) { return 0.0; }, [&](int i, double v) { ya[i] = v; });
   lane_batch<16>(ex, 0, nr, [&](int i) { return 0.0; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
-  kkt_solve<X, NX, NU>(ex, C, tA, ya, ra, x2, y, z2);
+  kkt_solve<X, NX, NU>(ex, C, tA, ya, ra, x2, y, z2, BMPC_NITREF_INIT);
   bring2cone(ex, C, z2, z);
   double tau = 1.0, kap = 1.0;
   const double resx0 = 1.0;   // max(1, ||c||), c = e_J
@@ -1658,11 +1664,14 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     bool ok = compute_scaling(ex, C, s, z);
     if (ok) ok = kkt_factor<X, NX, NU>(ex, C) && kkt_coupling<X, NX, NU>(ex, C);
     double alpha = 0.0, dtau = 0.0, dkap = 0.0;
+    // refinement only once the iterate nears the tolerances: an unrefined direction is
+    // accurate to ~1e-12 relative, far below what the early steps need
+    const int nref = score < BMPC_REFSCORE ? BMPC_NITREF : 0;
     if (ok) {
       // c vector
       lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
-      kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x1, y1, z1);
+      kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x1, y1, z1, nref);
       const double den = kap / tau - (x1[P.oJ] + vdot(ex, bv, y1, neq) + vdot(ex, hv, z1, nr));
       // affine: xi = -lam
       lane_batch<16>(ex, 0, nr, [&](int i) { return -lam[i]; }, [&](int i, double v) { ra[i] = v; });
@@ -1671,7 +1680,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nr, [&](int i) { return rz[i] - rb[i]; }, [&](int i, double v) { rb[i] = v; });
       lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
-      kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2);
+      kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2, nref);
       const double dk_aff = -kap * tau;
       const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
       lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
@@ -1701,7 +1710,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return -eta1 * rx[i]; }, [&](int i, double v) { tA[i] = v; });
       lane_batch(ex, 0, neq, [&](int i) { return eta1 * ry[i]; }, [&](int i, double v) { ya[i] = v; });
       ex.sync();
-      kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2);
+      kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2, nref);
       const double dk_c = -kap * tau - dtau_a * dkap_a + sigma * mu;
       dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
       lane_batch<16>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });

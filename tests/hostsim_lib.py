@@ -20,7 +20,10 @@ if PKG not in sys.path:
 
 from bmpc import abi  # noqa: E402
 
-SO = os.path.join(HERE, "hostsim", "libbmpc_hostsim.so")
+# BMPC_HOSTSIM_FLAGS: extra -D flags for algorithm experiments (a separate .so per flag set)
+FLAGS = os.environ.get("BMPC_HOSTSIM_FLAGS", "").split()
+SO = os.path.join(HERE, "hostsim", "libbmpc_hostsim%s.so" % (
+    "" if not FLAGS else "_" + "".join(c if c.isalnum() else "_" for c in "".join(FLAGS))[:80]))
 SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", "bmpc_plan.cpp")]
 HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")]
 
@@ -29,7 +32,7 @@ def build(force=False):
     newest = max(os.path.getmtime(p) for p in SRCS + HDRS + [os.path.join(REPO, "include", "bmpc.h")])
     if force or not os.path.exists(SO) or os.path.getmtime(SO) < newest:
         cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fopenmp", "-Wno-unknown-pragmas",
-               "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", SO]
+               *FLAGS, "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", SO]
         subprocess.check_call(cmd)
     return SO
 
