@@ -184,6 +184,9 @@ struct ProfScope {
 // loads of the batch are in flight together instead of one memory round trip per element
 // -- then commits them with st(i, v).  ld must not read what st of the same batch writes.
 // ------------------------------------------------------------------------------------
+// The loads are unconditional (an index past hi is clamped to b, which is valid): a load
+// under a per-lane guard would sit in its own exec-masked block with its own wait, i.e. one
+// memory round trip per element instead of one per batch.
 template <int UN = 8, class Ld, class St>
 BMPC_HD void strided_batch(int first, int stride, int hi, Ld ld, St st) {
   for (int b = first; b < hi; b += UN * stride) {
@@ -191,7 +194,7 @@ BMPC_HD void strided_batch(int first, int stride, int hi, Ld ld, St st) {
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int i = b + u * stride;
-      if (i < hi) v[u] = ld(i);
+      v[u] = ld(i < hi ? i : b);
     }
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
@@ -218,10 +221,9 @@ BMPC_HD double strided_partial(int first, int stride, int hi, F f) {
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int i = b + u * stride;
-      if (i < hi) {
-        const double v = f(i);
-        acc[u] = OP == 0 ? acc[u] + v : OP == 1 ? fmax(acc[u], v) : fmin(acc[u], v);
-      }
+      const double v = f(i < hi ? i : b);   // unconditional (see strided_batch)
+      const double r = OP == 0 ? acc[u] + v : OP == 1 ? fmax(acc[u], v) : fmin(acc[u], v);
+      acc[u] = i < hi ? r : acc[u];
     }
   }
   double s = init;

@@ -7,6 +7,7 @@
 // contiguous 512-byte segments.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -381,7 +382,13 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
-  const size_t lds_bytes = sizeof(double) * (size_t)P.nlds;
+  size_t lds_bytes = sizeof(double) * (size_t)P.nlds;
+  // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
+  // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
+  if (const char* e = getenv("BMPC_IPM_LDS_BYTES")) {
+    const size_t want = (size_t)atol(e);
+    if (want > lds_bytes && want <= 160 * 1024) lds_bytes = want;
+  }
   if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[0], s));
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,

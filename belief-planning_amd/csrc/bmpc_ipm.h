@@ -75,6 +75,41 @@ BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
   const int q = k >= 0 ? (P).t.cone_q[k] : 0
 
 // ------------------------------------------------------------------------------------
+// block of dot products in one pass: acc[a][b] = sum_i A_a[i] B_b[i] over the tree-variable
+// ranges [lo1, hi1) and [lo2, hi2), rows A_a = A + a*astr (a < na <= 4), B_b = B + b*bstr
+// (b < nb <= 4); every load of a lane's step is issued together (one round trip per pass
+// instead of one per dot product), then each entry is reduced over the wave.
+// ------------------------------------------------------------------------------------
+template <class X>
+BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const gdouble* B, size_t bstr, int nb,
+                        int lo1, int hi1, int lo2, int hi2, double (&acc)[4][4]) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+  const int n1 = hi1 - lo1, ntot = n1 + (hi2 - lo2);
+  auto idx = [&](int t) { return t < n1 ? lo1 + t : lo2 + (t - n1); };
+#pragma unroll 2
+  for (int t = ex.lane; t < ntot; t += ex.nlanes) {
+    const int i = idx(t);
+    double av[4], bv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) av[a] = a < na ? A[a * astr + i] : 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bv[b] = b < nb ? B[b * bstr + i] : 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += av[a] * bv[b];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (a < na && b < nb) acc[a][b] = ex.sum(acc[a][b]);
+}
+
+// ------------------------------------------------------------------------------------
 // reductions over one cone's rows, by the cone group G that owns the cone (k >= 0) or as an
 // idle member (k < 0, q = 0): every lane of the wave must make the same calls.
 // ------------------------------------------------------------------------------------
@@ -540,6 +575,7 @@ template <class X>
 BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out) {
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
+  BMPC_TIC(t_wlp);
   const gdouble* dl = C.at(C.L->dl);
   lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
@@ -550,6 +586,8 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
   const gdouble* a = C.at((mode == 0 || mode == 1) ? C.L->vnt : C.L->wbar);
   const bool jconj = (mode == 1 || mode == 3);
   constexpr int UC = 8;   // cone rows per lane held in registers between the two passes
+  BMPC_TOC(C.ws, *C.L, PROF_X1, t_wlp);
+  BMPC_TIC(t_wc);
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double e = k >= 0 ? eta[k] : 1.0;
@@ -583,7 +621,10 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
       }, [&](int i, double v) { out[off + i] = v; });
     }
   }
+  BMPC_TOC(C.ws, *C.L, PROF_X2, t_wc);
+  BMPC_TIC(t_ws);
   ex.sync();
+  BMPC_TOC(C.ws, *C.L, PROF_X3, t_ws);
 }
 
 // Jordan product out = u o v
@@ -959,6 +1000,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
   ex.sync();
 
   // ---- (2a) backward sweep (leaves -> root) ----------------------------------------------
+  BMPC_TIC(t_bw);
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
@@ -1072,6 +1114,7 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
     ex.sync();
   }
 
+  BMPC_TOC(C.ws, L, PROF_X4, t_bw);
   // ---- (2b) forward sweep (root -> leaves): x and u only ------------------------------------
   for (int it = ex.lane; it < nr; it += ex.nlanes) {
 #pragma unroll
@@ -1276,19 +1319,24 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
   const int ntree = P.oRho;    // x and u parts are [0, oRho); S part [oS, oJ)
   for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
   ex.sync();
-  // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables
-  for (int it = 0; it < nc * nc; ++it) {
-    const int k = it / nc, j = it % nc;
-    const gdouble* g = ws + L.gk + (size_t)k * P.nv;
-    const gdouble* col = ws + L.colk + (size_t)j * P.nv;
-    double s = lane_partial(ex, 0, ntree, [&](int i) { return g[i] * col[i]; }) +
-               lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * col[i]; });
-    s = ex.sum(s);
-    if (ex.lane == 0) {
-      const double ck = 2.0 / (eta[k] * eta[k]);
-      M[(ng + nb + k) * ns + ng + nb + j] = ck * s + (k == j ? 1.0 : 0.0);
+  // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables,
+  // 4 x 4 blocks of dot products per pass
+  for (int k0 = 0; k0 < nc; k0 += 4)
+    for (int j0 = 0; j0 < nc; j0 += 4) {
+      const int na = nc - k0 < 4 ? nc - k0 : 4, nbk = nc - j0 < 4 ? nc - j0 : 4;
+      double acc[4][4];
+      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, ws + L.colk + (size_t)j0 * P.nv, P.nv, nbk,
+                 0, ntree, P.oS, P.oJ, acc);
+      if (ex.lane == 0)
+        for (int a = 0; a < na; ++a) {
+          const int k = k0 + a;
+          const double ck = 2.0 / (eta[k] * eta[k]);
+          for (int b = 0; b < nbk; ++b) {
+            const int j = j0 + b;
+            M[(ng + nb + k) * ns + ng + nb + j] = ck * acc[a][b] + (k == j ? 1.0 : 0.0);
+          }
+        }
     }
-  }
   // H_gg diagonal: LP rows -rho, -mu+, -mu-
   for (int b = ex.lane; b < nb; b += ex.nlanes) {
     const double w = dl[P.rRisk + b];
@@ -1351,11 +1399,12 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   ldouble* b = ex.lds + P.lds_rhs;
   const gdouble* eta = ws + L.eta;
-  for (int k = 0; k < nc; ++k) {
-    const gdouble* g = ws + L.gk + (size_t)k * P.nv;
-    const double sk = ex.sum(lane_partial(ex, 0, P.oRho, [&](int i) { return g[i] * dx[i]; }) +
-                             lane_partial(ex, P.oS, P.oJ, [&](int i) { return g[i] * dx[i]; }));
-    if (ex.lane == 0) b[ng + nb + k] = 2.0 / (eta[k] * eta[k]) * sk;
+  for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
+    const int na = nc - k0 < 4 ? nc - k0 : 4;
+    double acc[4][4];
+    block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
+    if (ex.lane == 0)
+      for (int a = 0; a < na; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
   }
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
@@ -1425,14 +1474,12 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
     // e2 = r2 - A dx
     apply_A<X, NX, NU>(ex, C, dx, e2);
     lane_batch(ex, 0, P.neq, [&](int i) { return r2[i] - e2[i]; }, [&](int i, double v) { e2[i] = v; });
-    // e3 = r3h - W^-1 G dx + dzh
-    apply_G<X, NX, NU>(ex, C, dx, cz);
-    apply_W(ex, C, 1, cz, e3);
-    lane_batch<16>(ex, 0, P.nrows, [&](int i) { return r3h[i] - e3[i] + dz[i]; }, [&](int i, double v) { e3[i] = v; });
+    // e3 = r3h - W^-1 G dx + dzh is zero up to rounding: kkt_solve_once computed dzh as
+    // W^-1 G dx - r3h from the final dx with the same operators
+    lane_batch<16>(ex, 0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { e3[i] = v; });
     ex.sync();
-    const double err = ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(e1[i]); }),
-                                        strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(e2[i]); })),
-                                   strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(e3[i]); })));
+    const double err = ex.max(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(e1[i]); }),
+                                   strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(e2[i]); })));
 #ifdef BMPC_HOST_DEBUG
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
