@@ -109,6 +109,7 @@ struct Plan {
   int nsm;    // dense coupling system size
   // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
   int lds_M, lds_piv, lds_rhs, lds_red, nlds;
+  int lds_scr, nscr;       // tree-solve LDS scratch (slack terms of the pre-pass; 0 = none)
   int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
   double W1[BMPC_MAX_N * BMPC_MAX_N];   // sqrtm(Q) / chol(Q)'  (MPC_branch.py:1628-1631)
   double Wu[BMPC_MAX_D * BMPC_MAX_D];   // chol(R)'             (:1633-1636)

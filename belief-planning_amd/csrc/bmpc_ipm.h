@@ -25,6 +25,12 @@
 #ifndef BMPC_REFSCORE
 #define BMPC_REFSCORE 1e-3   // refine only when max(pres, dres, relgap) of the iterate < this (1e-4 flips replay exit codes)
 #endif
+#ifndef BMPC_REFSCORE2
+#define BMPC_REFSCORE2 1e-6  // ... and BMPC_NITREF2 rounds in the end game (score below this)
+#endif
+#ifndef BMPC_NITREF2
+#define BMPC_NITREF2 2
+#endif
 #ifndef BMPC_REFTOL
 #define BMPC_REFTOL 1e-14    // refinement stop: scaled residual <= tol * max(1, |rhs|) (oracle: 1e-14)
 #endif
@@ -575,7 +581,6 @@ template <class X>
 BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out) {
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
-  BMPC_TIC(t_wlp);
   const gdouble* dl = C.at(C.L->dl);
   lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
@@ -586,8 +591,6 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
   const gdouble* a = C.at((mode == 0 || mode == 1) ? C.L->vnt : C.L->wbar);
   const bool jconj = (mode == 1 || mode == 3);
   constexpr int UC = 8;   // cone rows per lane held in registers between the two passes
-  BMPC_TOC(C.ws, *C.L, PROF_X1, t_wlp);
-  BMPC_TIC(t_wc);
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double e = k >= 0 ? eta[k] : 1.0;
@@ -621,10 +624,7 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
       }, [&](int i, double v) { out[off + i] = v; });
     }
   }
-  BMPC_TOC(C.ws, *C.L, PROF_X2, t_wc);
-  BMPC_TIC(t_ws);
   ex.sync();
-  BMPC_TOC(C.ws, *C.L, PROF_X3, t_ws);
 }
 
 // Jordan product out = u o v
@@ -952,19 +952,57 @@ BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[N
   }
 }
 
+// one backward Riccati-sweep node of a task: g (successor terms, own rows) -> l, kf
+template <class X, int NX, int NU, int RX, int W>
+BMPC_HD void bw_node(const X& ex, int gl, const double (&qx)[RX], const double (&Acol)[RX][NX],
+                     const double (&Brow)[RX][NU], const double (&Kcol)[RX][NU], const double (&Lu)[NU][NU],
+                     const double (&ru)[NU], double (&g)[RX], double (&l)[RX], double (&kfv)[NU]) {
+#pragma unroll
+  for (int q = 0; q < RX; ++q)
+    if (gl * RX + q >= NX) g[q] = 0.0;
+  double gfull[NX];
+  task_gather<NX, RX, W>(ex, g, gfull);
+  // qu = -ru + B'g ;  kf = -Quu^-1 qu ;  l = qx0 + A'g + K'qu
+  double qu[NU];
+#pragma unroll
+  for (int m = 0; m < NU; ++m) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < RX; ++q) v += Brow[q][m] * g[q];
+    qu[m] = -ru[m] + ex.tsum(v);
+  }
+#pragma unroll
+  for (int m = 0; m < NU; ++m) kfv[m] = -qu[m];
+  chol_solve<NU>(Lu, kfv);
+#pragma unroll
+  for (int q = 0; q < RX; ++q) {
+    double v = qx[q];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) v += Acol[q][j] * gfull[j];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) v += Kcol[q][m] * qu[m];
+    l[q] = v;
+  }
+}
+
 // Tree solve of  [H_t A_dyn'; A_dyn 0] [v; nu] = [r; e]  for nr right-hand sides.
-// rhs r_i lives in z-space (x, u, S parts at P.oX/oU/oS), e_i in eq-space (first T*n rows;
-// pass Layout::zeros for none).  Solutions go to out_i (z-space tree parts) and nu_i
-// (eq-space, NULL skips).
+// rhs i: r_i = r0 + i*rs lives in z-space (x, u, S parts at P.oX/oU/oS), e_i = e0 + i*es in
+// eq-space (first T*n rows; Layout::zeros with es = 0 for none).  Solutions go to
+// o0 + i*os (z-space tree parts) and n0 + i*ns (eq-space multipliers; n0 = NULL skips).
+// Every vector lives in the ego's slab.
 // Structure: (1) lane-parallel pre-pass: slack elimination of every node's x rhs;
 // (2) the two sequential sweeps, one task per (branch, rhs) run by a group of
 // W = X::kTaskLanes lanes (a DPP quad on the GPU; lane gl owns state rows gl*RX..), carrying
 // the affine term l / the state x in registers along the branch -- only the Riccati data
 // is loaded per node; (3) lane-parallel post-pass: multipliers nu and slack recovery.
 template <class X, int NX, int NU>
-BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const* r,
-                        const gdouble* const* e, gdouble* const* out, gdouble* const* nu) {
+BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* r0, size_t rs, const gdouble* e0,
+                        size_t es, gdouble* o0, size_t os, gdouble* n0, size_t ns) {
   const Ctx C = Cin.uniform();
+  r0 = uniform_ptr(r0);
+  e0 = uniform_ptr(e0);
+  o0 = uniform_ptr(o0);
+  n0 = uniform_ptr(n0);
   constexpr int W = X::kTaskLanes;
   constexpr int RX = (NX + W - 1) / W;
   CPlan& P = *C.P;
@@ -978,44 +1016,65 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
   gdouble* q0_ = ws + L.qx0;    // [nr][T][NX]
   gdouble* kf_ = ws + L.kff;    // [nr][U][NU]
   const size_t lstr = (size_t)P.T * NX, kstr = (size_t)P.U * NU;
+  const size_t roff = (size_t)(r0 - ws), eoff = (size_t)(e0 - ws);
   const gdouble* dh = ws + L.dh;
   const gdouble* sdv = ws + L.sd;
   const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
 
   // ---- (1) pre-pass: qx0 = -r_x - sum_c f_c df r_S / sd (non-terminal nodes) -------------
+  // two flat passes (the slack terms a_kc into LDS scratch, then the node sums): a loop
+  // over c with loads inside would cost one round trip per c
+  ldouble* av = ex.lds + P.lds_scr;
+  const bool av_lds = P.nscr >= P.T * Nc;
   for (int ri = 0; ri < nr; ++ri) {
-    const gdouble* rr = r[ri];
+    const gdouble* rr = r0 + ri * rs;
     gdouble* q0 = q0_ + ri * lstr;
-    lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
-      const int k = it / NX, j = it % NX;
-      double v = -rr[P.oX + it];
-      if (t.x_u[k] >= 0)
+    if (av_lds) {
+      lane_batch<8>(ex, 0, P.T * Nc, [&](int it) {
+        const int k = it / Nc;
+        const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // terminal nodes add 0
+        return on * sdv[it * 2 + 1] * rr[P.oS + it] / sdv[it * 2];
+      }, [&](int it, double v) { av[it] = v; });
+      ex.sync();
+      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+        const int k = it / NX, j = it % NX;
+        double v = -rr[P.oX + it] + dh[it] * av[k * Nc];
+        for (int c = 1; c < Nc; ++c) v -= P.desc.Fx[(c - 1) * NX + j] * av[k * Nc + c];
+        return v;
+      }, [&](int it, double v) { q0[it] = v; });
+      ex.sync();
+    } else {
+      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+        const int k = it / NX, j = it % NX;
+        const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
+        double v = -rr[P.oX + it];
         for (int c = 0; c < Nc; ++c) {
           const double a = sdv[(k * Nc + c) * 2 + 1] * rr[P.oS + k * Nc + c] / sdv[(k * Nc + c) * 2];
-          v -= (c == 0 ? -dh[it] : P.desc.Fx[(c - 1) * NX + j]) * a;
+          v -= on * (c == 0 ? -dh[it] : P.desc.Fx[(c - 1) * NX + j]) * a;
         }
-      return v;
-    }, [&](int it, double v) { q0[it] = v; });
+        return v;
+      }, [&](int it, double v) { q0[it] = v; });
+    }
   }
   ex.sync();
 
   // ---- (2a) backward sweep (leaves -> root) ----------------------------------------------
-  BMPC_TIC(t_bw);
+  // The per-node loads do not depend on the recursion: one memory round trip per node.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
     const int rounds = (ntask + ngrp - 1) / ngrp;
+    const bool leaf = dep == P.NB;
     for (int rd = 0; rd < rounds; ++rd) {
       const int task = rd * ngrp + grp;
       if (task >= ntask) continue;       // whole group idle together
       const int b = b0 + task / nr, ri = task % nr;
-      const gdouble* rr = r[ri];
-      const gdouble* ee = e[ri];
+      const gdouble* rr = r0 + ri * rs;
+      const gdouble* ee = e0 + ri * es;
       gdouble* lvec = lv_ + ri * lstr;
       const gdouble* q0 = q0_ + ri * lstr;
       gdouble* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
-      const bool leaf = dep == P.NB;
       const int c0 = t.br_child0[b];
       double l[RX];
       if (leaf) {   // terminal node: l = -r_x (= qx0 there)
@@ -1029,7 +1088,6 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
       }
       for (int jn = len - 1; jn >= 0; --jn) {
         const int k = ndx + jn, u = ndu + jn;
-        // ---- loads (independent of the recursion) ----
         double qx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU];
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
@@ -1045,7 +1103,6 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
         mat_load(Lu, ws + L.Luu + u * NU * NU);
 #pragma unroll
         for (int m = 0; m < NU; ++m) ru[m] = rr[P.oU + u * NU + m];
-        // ---- g = sum over successors of (l_c + P_c e_c), own rows ----
         double g[RX];
         if (jn < len - 1 || leaf) {
           double ec[NX];
@@ -1077,34 +1134,12 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
             }
           }
         }
-#pragma unroll
-        for (int q = 0; q < RX; ++q)
-          if (gl * RX + q >= NX) g[q] = 0.0;
-        double gfull[NX];
-        task_gather<NX, RX, W>(ex, g, gfull);
-        // ---- qu = -ru + B'g ;  kf = -Quu^-1 qu ;  l = qx0 + A'g + K'qu ----
-        double qu[NU];
-#pragma unroll
-        for (int m = 0; m < NU; ++m) {
-          double v = 0.0;
-#pragma unroll
-          for (int q = 0; q < RX; ++q) v += Brow[q][m] * g[q];
-          qu[m] = -ru[m] + ex.tsum(v);
-        }
         double kfv[NU];
-#pragma unroll
-        for (int m = 0; m < NU; ++m) kfv[m] = -qu[m];
-        chol_solve<NU>(Lu, kfv);
+        bw_node<X, NX, NU, RX, W>(ex, gl, qx, Acol, Brow, Kcol, Lu, ru, g, l, kfv);
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q;
-          double v = qx[q];
-#pragma unroll
-          for (int j = 0; j < NX; ++j) v += Acol[q][j] * gfull[j];
-#pragma unroll
-          for (int m = 0; m < NU; ++m) v += Kcol[q][m] * qu[m];
-          l[q] = v;
-          if (i < NX) lvec[k * NX + i] = v;
+          if (i < NX) lvec[k * NX + i] = l[q];
         }
         if (gl == 0)
 #pragma unroll
@@ -1113,27 +1148,25 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
     }
     ex.sync();
   }
-
-  BMPC_TOC(C.ws, L, PROF_X4, t_bw);
   // ---- (2b) forward sweep (root -> leaves): x and u only ------------------------------------
-  for (int it = ex.lane; it < nr; it += ex.nlanes) {
-#pragma unroll
-    for (int j = 0; j < NX; ++j) out[it][P.oX + j] = e[it][j];
+  for (int it = ex.lane; it < nr * NX; it += ex.nlanes) {
+    const int ri = it / NX, j = it % NX;
+    o0[ri * os + P.oX + j] = e0[ri * es + j];
   }
   ex.sync();
   for (int dep = 0; dep <= P.NB; ++dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
     const int rounds = (ntask + ngrp - 1) / ngrp;
+    const bool leaf = dep == P.NB;
     for (int rd = 0; rd < rounds; ++rd) {
       const int task = rd * ngrp + grp;
       if (task >= ntask) continue;
       const int b = b0 + task / nr, ri = task % nr;
-      gdouble* o = out[ri];
-      const gdouble* ee = e[ri];
+      gdouble* o = o0 + ri * os;
+      const gdouble* ee = e0 + ri * es;
       const gdouble* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
-      const bool leaf = dep == P.NB;
       const int c0 = t.br_child0[b];
       double xk[NX];      // full state (every lane of the group holds all of it)
 #pragma unroll
@@ -1204,11 +1237,11 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
 
   // ---- (3) post-pass: nu_k = -(l_k + P_k x_k), slack recovery --------------------------------
   for (int ri = 0; ri < nr; ++ri) {
-    gdouble* o = out[ri];
-    const gdouble* rr = r[ri];
+    gdouble* o = o0 + ri * os;
+    const gdouble* rr = r0 + ri * rs;
     const gdouble* lvec = lv_ + ri * lstr;
-    if (nu[ri]) {
-      gdouble* nn = nu[ri];
+    if (n0) {
+      gdouble* nn = n0 + ri * ns;
       lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
         double v = lvec[it];
@@ -1219,11 +1252,11 @@ BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* const*
     }
     lane_batch<4>(ex, 0, P.T * Nc, [&](int it) {
       const int k = it / Nc, c = it % Nc;
+      const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
       double fx = 0.0;
-      if (t.x_u[k] >= 0)
 #pragma unroll
-        for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * o[P.oX + k * NX + j];
-      return (rr[P.oS + it] + sdv[it * 2 + 1] * fx) / sdv[it * 2];
+      for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * o[P.oX + k * NX + j];
+      return (rr[P.oS + it] + sdv[it * 2 + 1] * on * fx) / sdv[it * 2];
     }, [&](int it, double v) { o[P.oS + it] = v; });
   }
   ex.sync();
@@ -1300,17 +1333,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
   BMPC_PROF(C.ws, L, PROF_COUPLING);
   gdouble* ws = C.ws;
   const int nc = P.ncones;
-  const gdouble* rr[32];
-  const gdouble* ee[32];
-  gdouble* oo[32];
-  gdouble* nn[32];
-  for (int k = 0; k < nc; ++k) {
-    rr[k] = ws + L.gk + (size_t)k * P.nv;
-    ee[k] = ws + L.zeros;
-    oo[k] = ws + L.colk + (size_t)k * P.nv;
-    nn[k] = ws + L.colnu + (size_t)k * P.neq;
-  }
-  tree_solve<X, NX, NU>(ex, C, nc, rr, ee, oo, nn);
+  tree_solve<X, NX, NU>(ex, C, nc, ws + L.gk, P.nv, ws + L.zeros, 0, ws + L.colk, P.nv, ws + L.colnu, P.neq);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
   ldouble* M = ex.lds + P.lds_M;
   const gdouble* eta = ws + L.eta;
@@ -1389,13 +1412,7 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-1 r3h
   lane_batch<16>(ex, 0, P.nv, [&](int i) { return tz[i] + r1[i]; }, [&](int i, double v) { tz[i] = v; });
   ex.sync();
-  {
-    const gdouble* rr[1] = {tz};
-    const gdouble* ee[1] = {r2};
-    gdouble* oo[1] = {dx};
-    gdouble* nn[1] = {dy};
-    tree_solve<X, NX, NU>(ex, C, 1, rr, ee, oo, nn);
-  }
+  tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   ldouble* b = ex.lds + P.lds_rhs;
   const gdouble* eta = ws + L.eta;
@@ -1713,7 +1730,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     double alpha = 0.0, dtau = 0.0, dkap = 0.0;
     // refinement only once the iterate nears the tolerances: an unrefined direction is
     // accurate to ~1e-12 relative, far below what the early steps need
-    const int nref = score < BMPC_REFSCORE ? BMPC_NITREF : 0;
+    const int nref = score < BMPC_REFSCORE2 ? BMPC_NITREF2 : score < BMPC_REFSCORE ? BMPC_NITREF : 0;
     if (ok) {
       // c vector
       lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });

@@ -1,4 +1,5 @@
 // bmpc_plan.cpp -- host-side plan construction (see bmpc_plan.h).
+#include <stdlib.h>
 #include "bmpc_plan.h"
 
 #include <math.h>
@@ -292,6 +293,11 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
     P.lds_M = P.lds_piv = P.lds_rhs = P.lds_red = 0;
     P.nlds = 64;
   }
+  // tree-solve scratch (CVaR IPM): the pre-pass slack terms, T * Nc doubles, while the
+  // per-workgroup LDS stays within 9,984 bytes (16 egos per CU)
+  P.lds_scr = P.nlds;
+  P.nscr = desc.controller == BMPC_CTRL_CVAR && P.nlds + T * P.Nc <= 1248 ? T * P.Nc : 0;
+  P.nlds += P.nscr;
 
   // ---- weights -----------------------------------------------------------------------------
   double Qm[BMPC_MAX_N * BMPC_MAX_N], Rm[BMPC_MAX_D * BMPC_MAX_D];

@@ -1,5 +1,6 @@
+# development experiment driver (GPU box): A/B of the LDS-staged tree sweeps
 set -e
-timeout -k 10 200 python tools/replay_diag.py > gpurun_out/diag.log 2>&1
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
-timeout -k 10 200 python tools/quick_bench.py 4096 2>&1 | grep "^step" > gpurun_out/qb.log
-BMPC_LIBRARY=belief-planning_amd/libbmpc_prof.so timeout -k 10 200 python tools/phase_profile.py 4096 > gpurun_out/ph.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 200 python tools/quick_bench.py 4096 > gpurun_out/qb.log 2>&1
+BMPC_NO_STAGE=1 timeout -k 10 200 python tools/quick_bench.py 4096 > gpurun_out/qb_nostage.log 2>&1
+timeout -k 10 200 python tools/quick_bench.py 4096 > gpurun_out/qb2.log 2>&1
