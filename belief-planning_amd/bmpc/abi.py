@@ -41,6 +41,28 @@ class PlanDesc(C.Structure):
     ]
 
 
+ENV_STRIDE, ENV_NSTAT = 16, 8
+# scene state / statistics slots (bmpc_env.h)
+ENV_X, ENV_Z, ENV_UOBS, ENV_LANE0, ENV_LANE1, ENV_COLL, ENV_OBSPOL, ENV_STEPS = 0, 4, 8, 10, 11, 12, 13, 14
+ENVS_J, ENVS_J2, ENVS_INFEAS, ENVS_ITERS, ENVS_SOLVES, ENVS_COLL_STEPS, ENVS_COLLIDED = range(7)
+
+
+class EnvDesc(C.Structure):
+    """bmpc_env_desc: the sim_overtake scene (Highway_env_branch.py:46-72)."""
+    _fields_ = [("n_lane", C.c_int32), ("reserved", C.c_int32), ("L", C.c_double), ("W", C.c_double),
+                ("Kpsi", C.c_double), ("v0", C.c_double), ("vlen", C.c_double), ("vwid", C.c_double),
+                ("target", C.c_double * 4)]
+
+
+def make_env(n_lane=4, L=4.0, W=2.5, Kpsi=0.1, v0=20.0, target=(0.5, 1.8, 15.0, 0.0), vlen=4.0, vwid=2.4):
+    """Scene constants of main_branch.sim_overtake: Branch_constants (main_branch.py:37), the
+    construction-time lane-change target xRef (:39), vehicle() size (Highway_env_branch.py:29)."""
+    E = EnvDesc()
+    E.n_lane, E.L, E.W, E.Kpsi, E.v0, E.vlen, E.vwid = int(n_lane), L, W, Kpsi, v0, vlen, vwid
+    _fill(E.target, target)
+    return E
+
+
 def _fill(arr, values):
     v = np.asarray(values, dtype=np.float64).ravel()
     for i, x in enumerate(v):

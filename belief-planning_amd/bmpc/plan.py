@@ -79,10 +79,21 @@ class BatchPlan:
 
     def solve_device(self, x_ptr, z_ptr, xref_ptr, upred_ptr=None, xpred_ptr=None, bw_ptr=None,
                      J_ptr=None, status_ptr=None, iters_ptr=None, stream=None):
-        """Device-pointer variant (e.g. torch tensors' data_ptr()), asynchronous."""
+        """Device-pointer variant (e.g. torch tensors' data_ptr()), asynchronous, enqueued on
+        `stream` (a hipStream_t handle; None = the plan's own non-blocking stream, which is
+        NOT ordered with the legacy default stream -- pass the caller's stream)."""
         vp = [C.c_void_p(p) if p else None for p in (x_ptr, z_ptr, xref_ptr, upred_ptr, xpred_ptr,
                                                      bw_ptr, J_ptr, status_ptr, iters_ptr, stream)]
         check(lib().bmpc_solve_device(self._h, *vp), "bmpc_solve_device")
+
+    def env_step_device(self, env: abi.EnvDesc, t: int, scene_ptr, upred_ptr, x_ptr, z_ptr, xref_ptr,
+                        J_ptr=None, status_ptr=None, iters_ptr=None, stats_ptr=None, stream=None):
+        """One closed-loop sim_overtake step of every ego on the device (bmpc_env_step):
+        Euler step with the last uPred[0], collision flag, obstacle backup choice, lane /
+        lane-change-target bookkeeping and x_ref -> the next solve's x, z, xref.  Async."""
+        vp = [C.c_void_p(p) if p else None for p in (scene_ptr, upred_ptr, J_ptr, status_ptr, iters_ptr,
+                                                     x_ptr, z_ptr, xref_ptr, stats_ptr, stream)]
+        check(lib().bmpc_env_step(self._h, C.byref(env), int(t), *vp), "bmpc_env_step")
 
     def get_warm_start(self):
         """Checkpoint of the per-ego warm start (uLin, p, Jcons, OldInput)."""

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "bmpc_plan.h"
+#include "bmpc_env.h"
 #include "bmpc_hmm.h"
 #include "bmpc_qp.h"
 #include "bmpc_solve.h"
@@ -152,6 +153,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   }
 }
 
+// one thread per ego: the closed-loop scene step (bmpc_env.h) around the solve
+__global__ void k_env(bmpc_env_desc E, double dt, int N, int m, int U, int d, int t, int batch, double* scene,
+                      bmpc_policy* pol, const double* upred, const double* J, const int32_t* status,
+                      const int32_t* iters, int cvar, double* x, double* z, double* xref, double* stats) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= batch) return;
+  double* st = scene + (size_t)e * ENV_STRIDE;
+  if (t > 0 && stats && J && status && iters)
+    env_accumulate(st, J[e], status[e], iters[e], cvar != 0, stats + (size_t)e * ENVS_STRIDE);
+  env_step_ego(E, dt, N, m, t, st, pol + (size_t)e * m, upred ? upred + (size_t)e * U * d : nullptr,
+               x + (size_t)e * 4, z + (size_t)e * 4, xref + (size_t)e * 4);
+}
+
 __global__ void k_gather(const double* __restrict__ ws, size_t stride, size_t off, int count,
                          double* __restrict__ out, int batch) {
   const size_t tot = (size_t)batch * count;
@@ -240,6 +254,7 @@ struct bmpc_plan {
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   double t_acc[2] = {0, 0};
   int t_cnt = 0;
+  bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
 };
 
 extern "C" {
@@ -351,10 +366,16 @@ int bmpc_plan_info(const bmpc_plan* pl, int32_t* info) {
 int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask) {
   if (!pl || !pol) return fail(-22, "null argument");
   const int m = pl->hp.plan.m;
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  if (pl->pol_on_device && mask) {   // keep the device-side re-targets of unmasked egos
+    HIPCHECK(hipStreamSynchronize(pl->stream));
+    if (pl->user_stream) HIPCHECK(hipStreamSynchronize(pl->user_stream));
+    HIPCHECK(hipMemcpy(pl->h_pol.data(), pl->d_pol, sizeof(bmpc_policy) * pl->h_pol.size(), hipMemcpyDeviceToHost));
+  }
+  pl->pol_on_device = false;
   for (int e = 0; e < pl->batch; ++e)
     if (!mask || mask[e])
       memcpy(&pl->h_pol[(size_t)e * m], pol + (size_t)e * m, sizeof(bmpc_policy) * m);
-  HIPCHECK(hipSetDevice(pl->ctx->device));
   HIPCHECK(hipMemcpyAsync(pl->d_pol, pl->h_pol.data(), sizeof(bmpc_policy) * pl->h_pol.size(),
                           hipMemcpyHostToDevice, pl->stream));
   HIPCHECK(hipStreamSynchronize(pl->stream));
@@ -457,6 +478,26 @@ int bmpc_solve_device(bmpc_plan* pl, const double* d_x, const double* d_z, const
   HIPCHECK(hipSetDevice(pl->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
   return launch_solve(pl, d_x, d_z, d_xref, d_upred, d_xpred, d_branch_w, d_J, d_status, d_iters, s);
+}
+
+int bmpc_env_step(bmpc_plan* pl, const bmpc_env_desc* env, int t, double* d_scene, const double* d_upred,
+                  const double* d_J, const int32_t* d_status, const int32_t* d_iters, double* d_x,
+                  double* d_z, double* d_xref, double* d_stats, void* stream) {
+  if (!pl || !env || !d_scene || !d_x || !d_z || !d_xref) return fail(-22, "null argument");
+  const Plan& P = pl->hp.plan;
+  if (P.desc.model != BMPC_MODEL_HIGHWAY || P.n != 4 || P.d != 2)
+    return fail(-22, "bmpc_env_step: the overtake scene needs a highway plan (n = 4, d = 2)");
+  if (t < 0 || (t > 0 && !d_upred)) return fail(-22, "bmpc_env_step: t > 0 needs the last uPred");
+  if (env->n_lane < 1) return fail(-22, "bmpc_env_step: n_lane < 1");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
+  if (stream) pl->user_stream = s;
+  hipLaunchKernelGGL(k_env, dim3((pl->batch + 63) / 64), dim3(64), 0, s, *env, P.desc.dt, P.N, P.m, P.U, P.d, t,
+                     pl->batch, d_scene, pl->d_pol, d_upred, d_J, d_status, d_iters,
+                     P.desc.controller == BMPC_CTRL_CVAR ? 1 : 0, d_x, d_z, d_xref, d_stats);
+  HIPCHECK(hipGetLastError());
+  pl->pol_on_device = true;
+  return 0;
 }
 
 static int gather(bmpc_plan* pl, size_t off, int count, double* host) {

@@ -134,7 +134,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from bmpc import plan
+    from bmpc import abi, plan
     from bmpc.scenarios import (highway_desc, highway_policy_rows, quadruped_desc, quadruped_policy_rows,
                                 seeded_batch, seeded_quadruped_batch)
 
@@ -163,34 +163,24 @@ def main():
     Jv = torch.zeros(B, device=dev, dtype=torch.float64)
     st = torch.zeros(B, device=dev, dtype=torch.int32)
     it = torch.zeros(B, device=dev, dtype=torch.int32)
-    stats = torch.zeros(D.NSTAT, device=dev, dtype=torch.float64)
-    stream = torch.cuda.current_stream(dev)
-    dt, v0 = 0.1, 20.0
+    # one dedicated stream: the library's kernels and torch's ops run in order on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sh = stream.cuda_stream
+    env = abi.make_env()                       # main_branch.sim_overtake scene constants
+    scene = torch.zeros((B, abi.ENV_STRIDE), device=dev, dtype=torch.float64)
+    scene[:, 0:4] = tx
+    scene[:, 4:8] = tz
+    estats = torch.zeros((B, abi.ENV_NSTAT), device=dev, dtype=torch.float64)
+    tstep = [0]
 
     def env_step():
-        """Euler step of ego (uPred[0]) and obstacle (maintain policy) + x_ref rule
-        (Highway_env_branch.py:39-41,153-167), on device."""
-        u0 = up[:, 0, :]
-        xs = tx
-        tx.copy_(xs + dt * torch.stack([xs[:, 2] * torch.cos(xs[:, 3]), xs[:, 2] * torch.sin(xs[:, 3]),
-                                         u0[:, 0], u0[:, 1]], 1))
-        zs = tz
-        tz.copy_(zs + dt * torch.stack([zs[:, 2] * torch.cos(zs[:, 3]), zs[:, 2] * torch.sin(zs[:, 3]),
-                                         torch.zeros_like(zs[:, 0]), -0.1 * zs[:, 3]], 1))
-        lane0 = torch.round((tx[:, 1] - 1.8) / 3.6)
-        Ydes = torch.where(tx[:, 0] < tz[:, 0], 1.8 + lane0 * 3.6, tz[:, 1])
-        vdes = torch.where((torch.abs(tx[:, 1] - Ydes) < 1) & (tx[:, 0] > tz[:, 0] + 3),
-                           torch.full_like(Ydes, v0), tz[:, 2] + (tz[:, 0] + 1.5 - tx[:, 0]))
-        tr[:, 1] = Ydes
-        tr[:, 2] = vdes
-        # closed-loop statistics (Highway_sim collision rule :421-429)
-        dis = torch.maximum(torch.abs(tx[:, 0] - tz[:, 0]) - 4.0, torch.abs(tx[:, 1] - tz[:, 1]) - 2.4)
-        stats[D.STAT_J] += Jv.sum()
-        stats[D.STAT_J2] += (Jv * Jv).sum()
-        stats[D.STAT_INFEAS] += (st < 0).sum()
-        stats[D.STAT_ITERS] += it.sum()
-        stats[D.STAT_SOLVES] += B
-        stats[D.STAT_COLL] += (dis < 0).sum()
+        """Highway_env.step around the solve, on the device (k_env): Euler steps with
+        uPred[0], collision flag, obstacle backup argmax, lane bookkeeping / lane-change
+        re-targeting, x_ref rule (Highway_env_branch.py:83-184, :421-429)."""
+        pl.env_step_device(env, tstep[0], scene.data_ptr(), up.data_ptr(), tx.data_ptr(), tz.data_ptr(),
+                           tr.data_ptr(), Jv.data_ptr(), st.data_ptr(), it.data_ptr(), estats.data_ptr(), sh)
+        tstep[0] += 1
 
     qdt, qv0 = 0.2, 0.2
     xdes = torch.tensor([5.0, -3.0, 0.0], device=dev, dtype=torch.float64)
@@ -211,22 +201,25 @@ def main():
         tr[:, 0:2] = tx[:, 0:2] + dxy
         tr[:, 2] = psi
         dis = torch.linalg.norm(tx[:, 0:2] - tz[:, 0:2], dim=1) - 0.75
-        stats[D.STAT_J] += Jv.sum()
-        stats[D.STAT_J2] += (Jv * Jv).sum()
-        stats[D.STAT_INFEAS] += (st != 1).sum()
-        stats[D.STAT_ITERS] += it.sum()
-        stats[D.STAT_SOLVES] += B
-        stats[D.STAT_COLL] += (dis < 0).sum()
+        estats[:, abi.ENVS_J] += Jv
+        estats[:, abi.ENVS_J2] += Jv * Jv
+        estats[:, abi.ENVS_INFEAS] += (st != 1).double()
+        estats[:, abi.ENVS_ITERS] += it.double()
+        estats[:, abi.ENVS_SOLVES] += 1.0
+        estats[:, abi.ENVS_COLL_STEPS] += (dis < 0).double()
 
     def step():
+        # one closed-loop step: scene update -> solve (inputs / outputs stay in HBM)
+        if not quad:
+            env_step()
         pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
-                        Jv.data_ptr(), st.data_ptr(), it.data_ptr(), stream.cuda_stream)
-        quad_env_step() if quad else env_step()
+                        Jv.data_ptr(), st.data_ptr(), it.data_ptr(), sh)
+        if quad:
+            quad_env_step()
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    stats.zero_()
     # per-kernel device timing over separate instrumented steps (HIP events on the launch
     # stream); the timed region below runs without event synchronisation
     pl.enable_timing(True)
@@ -235,13 +228,14 @@ def main():
     tm = pl.timing()
     pl.enable_timing(False)
     iters_mean = float(it.double().mean().item())
-    stats.zero_()
+    estats.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    stats = estats.sum(0)
     D.reduce_stats(stats)        # the only collective
     torch.cuda.synchronize()
     if world > 1:
@@ -280,10 +274,12 @@ def main():
                          "tree_kernel_ms": round(tm["tree_ms"], 4),
                          "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
                          "flop_model_per_solve": F_mod},
-            "closed_loop": {"J_mean": float(st_h[D.STAT_J] / max(st_h[D.STAT_SOLVES], 1)),
-                            "infeasible": int(st_h[D.STAT_INFEAS]),
-                            "iters_mean": float(st_h[D.STAT_ITERS] / max(st_h[D.STAT_SOLVES], 1)),
-                            "collision_steps": int(st_h[D.STAT_COLL])},
+            "closed_loop": {"J_mean": float(st_h[abi.ENVS_J] / max(st_h[abi.ENVS_SOLVES], 1)),
+                            "infeasible": int(st_h[abi.ENVS_INFEAS]),
+                            "iters_mean": float(st_h[abi.ENVS_ITERS] / max(st_h[abi.ENVS_SOLVES], 1)),
+                            "solves": int(st_h[abi.ENVS_SOLVES]),
+                            "collision_steps": int(st_h[abi.ENVS_COLL_STEPS]),
+                            "env": "device k_env (sim_overtake scene)" if not quad else "torch ops"},
         }
         if not a.no_cpu_baseline and world == 1 and not quad:
             procs = max(1, min(8, len(os.sched_getaffinity(0))))

@@ -20,6 +20,8 @@
  *   bmpc_get_tree      <- BranchTree fields + BT2array    MPC_branch.py:65-78,2108-2122
  *   bmpc_model_eval    <- PredictiveModel.dyn_linearization / branch_eval / zpred_eval /
  *                         col_eval                         highway_branch_dyn.py:284-325
+ *   bmpc_env_step      <- Highway_env.step + Highway_sim collision rule
+ *                                                          Highway_env_branch.py:83-184,421-429
  *
  * Conventions: all host buffers are caller-owned, C-contiguous, ego-major, float64
  * (int32 for status/iteration counts).  Return codes are 0 on success and a negative
@@ -195,6 +197,34 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
                     int B, const double* x, const double* u, const double* z,
                     double* A, double* Bm, double* C, double* xp, double* p, double* dp,
                     double* zpred, double* h0, double* dh);
+
+/* Closed-loop sim_overtake scene on the device, one scene per ego of a highway plan:
+ * replaces Highway_env_branch.Highway_env.step (Highway_env_branch.py:83-184) around the
+ * solve and the collision rule of Highway_sim (:421-429).  */
+#define BMPC_ENV_STRIDE 16  /* doubles of per-ego scene state  */
+#define BMPC_ENV_NSTAT 8    /* doubles of per-ego statistics   */
+typedef struct {
+  int32_t n_lane;     /* lanes of the env (LB = [W/2, n_lane*3.6 - W/2], :64); 4 in sim_overtake */
+  int32_t reserved;
+  double L, W, Kpsi;  /* Branch_constants (main_branch.py:37)                        */
+  double v0;          /* 20 (Highway_env_branch.py:22)                               */
+  double vlen, vwid;  /* vehicle() size 4 x 2.4 (:29), used by the collision test    */
+  double target[4];   /* lane-change target of the env's construction-time backup list */
+} bmpc_env_desc;
+
+/* One closed-loop step t of every ego (device pointers, enqueued on `stream`):
+ *   scene  [batch][BMPC_ENV_STRIDE]  state: ego x[0..3], obstacle z[4..7], the rest zero at
+ *                                    t = 0 (the caller writes the initial states);
+ *   upred  [batch][U][d]             the last solve's uPred (ignored at t = 0);
+ *   J, status, iters [batch]         the last solve's outputs for the statistics (NULL skips);
+ *   x, z, xref [batch][4]            out: the next solve's inputs;
+ *   stats  [batch][BMPC_ENV_NSTAT]   accumulated {sum J, sum J^2, infeasible, iterations,
+ *                                    solves, steps in collision, collided} (NULL skips).
+ * The plan's lane-change policies are re-targeted on the device (update_backup, :118). */
+int bmpc_env_step(bmpc_plan* plan, const bmpc_env_desc* env, int t, double* d_scene,
+                  const double* d_upred, const double* d_J, const int32_t* d_status,
+                  const int32_t* d_iters, double* d_x, double* d_z, double* d_xref,
+                  double* d_stats, void* stream);
 
 /* HMM belief-augmented linearisation, batched over B points: replaces
  * HMM_backup_dyn.PredictiveModel.regressionAndLinearization (HMM_backup_dyn.py:216-237) of

@@ -13,6 +13,7 @@
 #include "bmpc_plan.h"
 #include "bmpc_hmm.h"
 #include "bmpc_solve.h"
+#include "bmpc_env.h"
 
 using namespace bmpc;
 
@@ -192,6 +193,27 @@ int hs_model_eval(const bmpc_plan_desc* D, const bmpc_policy* pol, int B, const 
   return 0;
 }
 
+
+int hs_env_step(void* p, const bmpc_env_desc* env, int t, double* scene, const double* upred, const double* J,
+                const int32_t* status, const int32_t* iters, double* x, double* z, double* xref, double* stats) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  for (int e = 0; e < h->batch; ++e) {
+    double* st = scene + (size_t)e * ENV_STRIDE;
+    if (t > 0 && stats && J && status && iters)
+      env_accumulate(st, J[e], status[e], iters[e], P.desc.controller == BMPC_CTRL_CVAR, stats + (size_t)e * ENVS_STRIDE);
+    env_step_ego(*env, P.desc.dt, P.N, P.m, t, st, h->pol.data() + (size_t)e * P.m,
+                 upred ? upred + (size_t)e * P.U * P.d : nullptr, x + (size_t)e * 4, z + (size_t)e * 4,
+                 xref + (size_t)e * 4);
+  }
+  return 0;
+}
+
+int hs_get_policies(void* p, bmpc_policy* out) {
+  HS* h = (HS*)p;
+  memcpy(out, h->pol.data(), sizeof(bmpc_policy) * h->pol.size());
+  return 0;
+}
 
 int hs_hmm_eval(int M, int m, const double* hc, int B, const double* xb, const double* u, const double* xbackup,
                 double* xbp, double* A, double* Bm, double* C, double* h0, double* Jh) {

@@ -88,6 +88,20 @@ class HostSim:
         lib().hs_solve(self.h, _p(x), _p(z), _p(xref), _p(up), _p(xp), _p(bw), _p(J), _p(st), _p(it))
         return dict(upred=up, xpred=xp, branch_w=bw, J=J, status=st, iters=it)
 
+    def env_step(self, env, t, scene, upred=None, J=None, status=None, iters=None, stats=None):
+        """Host build of bmpc_env_step: advances `scene` [B][16] in place, returns x, z, xref."""
+        B = self.batch
+        x, z, xref = np.zeros((B, 4)), np.zeros((B, 4)), np.zeros((B, 4))
+        up = None if upred is None else np.ascontiguousarray(np.asarray(upred, float).reshape(B, self.U, self.desc.d))
+        lib().hs_env_step(self.h, C.byref(env), int(t), _p(scene), _p(up), _p(J), _p(status), _p(iters),
+                          _p(x), _p(z), _p(xref), _p(stats))
+        return x, z, xref
+
+    def get_policies(self):
+        arr = (abi.Policy * (self.batch * self.desc.m))()
+        lib().hs_get_policies(self.h, arr)
+        return arr
+
     def set_warm_start(self, uLin, pprev, jcons=None, oldu=None):
         B = self.batch
         uLin = np.ascontiguousarray(np.asarray(uLin, float).reshape(B, self.U + 1, self.desc.d))
