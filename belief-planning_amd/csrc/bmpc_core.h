@@ -17,7 +17,11 @@
 #define BMPC_HD __host__ __device__ __forceinline__
 // phase-sized functions stay out of line: the IPM kernel calls them from many sites and
 // inlining them all blows the kernel past the instruction cache
+#if defined(BMPC_INLINE_ALL)
+#define BMPC_FN __host__ __device__ __forceinline__
+#else
 #define BMPC_FN __host__ __device__ __attribute__((noinline))
+#endif
 #else
 #define BMPC_HD inline
 #define BMPC_FN inline

@@ -262,10 +262,13 @@ BMPC_FN void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out)
   ex.sync();
 }
 
-// out(nv) = G' r
+// out(nv) = G' r (+ add, when add is not NULL)
 template <class X, int NX, int NU>
-BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out) {
+BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out, const gdouble* add = nullptr) {
   const Ctx C = Cin.uniform();
+  add = uniform_ptr(add);
+  const double sa = add ? 1.0 : 0.0;
+  const gdouble* ad = add ? add : r;   // read and scaled by 0 without an addend
   double qx[NX];
   ctx_qx<NX>(C, qx);
   CPlan& P = *C.P;
@@ -309,9 +312,9 @@ BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out)
         for (int j = 0; j < NX; ++j) ax[j] += (c == 0 ? -dhk[j] : P.desc.Fx[(c - 1) * NX + j]) * rv;
       os[c] = -rv - r[P.rPos + k * Nc + c] + fS;
     }
-    for (int c = 0; c < Nc; ++c) out[P.oS + k * Nc + c] = os[c];
+    for (int c = 0; c < Nc; ++c) out[P.oS + k * Nc + c] = os[c] + sa * ad[P.oS + k * Nc + c];
 #pragma unroll
-    for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = kc >= 0 ? ax[j] + cx[j] : ax[j];
+    for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = (kc >= 0 ? ax[j] + cx[j] : ax[j]) + sa * ad[P.oX + k * NX + j];
   }
   // input nodes
   for (int u = ex.lane; u < P.U; u += ex.nlanes) {
@@ -337,7 +340,7 @@ BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out)
       }
     }
 #pragma unroll
-    for (int j = 0; j < NU; ++j) out[P.oU + u * NU + j] = au[j];
+    for (int j = 0; j < NU; ++j) out[P.oU + u * NU + j] = au[j] + sa * ad[P.oU + u * NU + j];
   }
   // globals: one lane per global variable, gathering its cone and risk-row terms
   for (int i = ex.lane; i < P.ng; i += ex.nlanes) {
@@ -360,7 +363,7 @@ BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out)
       }
       if (w != 0.0) v += w * (r[off] - r[off + q - 1]) * exp(-boost[k]);
     }
-    out[gi] = v;
+    out[gi] = v + sa * ad[gi];
   }
   ex.sync();
 }
@@ -576,15 +579,21 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   ex.sync();
 }
 
+// out = sw * W_mode in + sa * add   (add may be NULL; in == out allowed: every output row
+// depends on its own input row and its cone's dot product, read before any write)
 // mode 0: W v, 1: W^-1 v, 2: W^2 v, 3: W^-2 v   (W symmetric NT scaling)
 template <class X>
-BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out) {
+BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out, double sw = 1.0,
+                     const gdouble* add = nullptr, double sa = 0.0) {
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
   const gdouble* dl = C.at(C.L->dl);
+  const gdouble* ad = add ? add : in;   // read and scaled by 0 without an addend
+  if (!add) sa = 0.0;
   lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
-    return mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
+    const double v = mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
+    return sw * v + sa * ad[i];
   }, [&](int i, double v) { out[i] = v; });
   const gdouble* eta = C.at(C.L->eta);
   // W = e (2 v v' - J); W^-1 = (2 Jv Jv' - J)/e; W^2 = e^2 (2 wb wb' - J); W^-2 = (2 Jwb Jwb' - J)/e^2
@@ -594,7 +603,7 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double e = k >= 0 ? eta[k] : 1.0;
-    const double sc = mode == 0 ? e : mode == 1 ? 1.0 / e : mode == 2 ? e * e : 1.0 / (e * e);
+    const double sc = sw * (mode == 0 ? e : mode == 1 ? 1.0 / e : mode == 2 ? e * e : 1.0 / (e * e));
     const double in0 = q > 0 ? in[off] : 0.0;
     if (q <= UC * G.cg) {   // one pass: the cone's rows stay in registers
       double av[UC], iv[UC];
@@ -607,10 +616,16 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
         part += av[uu] * iv[uu];
       }
       const double dot = ex.gsum(part, G.cg);
+      double adv[UC];
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
         const int i = G.gl + uu * G.cg;
-        if (i < q) out[off + i] = sc * (2.0 * av[uu] * dot - (i == 0 ? in0 : -iv[uu]));
+        adv[uu] = i < q ? ad[off + i] : 0.0;
+      }
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = G.gl + uu * G.cg;
+        if (i < q) out[off + i] = sc * (2.0 * av[uu] * dot - (i == 0 ? in0 : -iv[uu])) + sa * adv[uu];
       }
     } else {                // long cones: dot pass, then write pass
       const double dot = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
@@ -620,7 +635,7 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
       strided_batch<4>(G.gl, G.cg, q, [&](int i) {
         const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
         const double jv = i == 0 ? in0 : -in[off + i];
-        return sc * (2.0 * ai * dot - jv);
+        return sc * (2.0 * ai * dot - jv) + sa * ad[off + i];
       }, [&](int i, double v) { out[off + i] = v; });
     }
   }
@@ -1409,9 +1424,7 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   gdouble* tr = ws + L.k_r0;
   gdouble* tz = ws + L.k_nv0;
   apply_W(ex, C, 1, r3h, tr);                     // W^-1 r3h
-  apply_GT<X, NX, NU>(ex, C, tr, tz);             // G' W^-1 r3h
-  lane_batch<16>(ex, 0, P.nv, [&](int i) { return tz[i] + r1[i]; }, [&](int i, double v) { tz[i] = v; });
-  ex.sync();
+  apply_GT<X, NX, NU>(ex, C, tr, tz, r1);         // G' W^-1 r3h + r1
   tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   ldouble* b = ex.lds + P.lds_rhs;
@@ -1449,9 +1462,7 @@ BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   ex.sync();
   // dzh = W^-1 G dx - r3h
   apply_G<X, NX, NU>(ex, C, dx, tr);
-  apply_W(ex, C, 1, tr, dzh);
-  lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dzh[i] - r3h[i]; }, [&](int i, double v) { dzh[i] = v; });
-  ex.sync();
+  apply_W(ex, C, 1, tr, dzh, 1.0, r3h, -1.0);
 }
 
 // Solve [0 A' G'; A 0 0; G 0 -W^2] [dx; dy; dz] = [r1; r2; r3]: W-scaled solve with
@@ -1507,10 +1518,8 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
     lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[i] + cz[i]; }, [&](int i, double v) { dz[i] = v; });
     ex.sync();
   }
-  // dz = W^-1 dzh
-  apply_W(ex, C, 1, dz, e3);
-  lane_batch<16>(ex, 0, P.nrows, [&](int i) { return e3[i]; }, [&](int i, double v) { dz[i] = v; });
-  ex.sync();
+  // dz = W^-1 dzh (in place)
+  apply_W(ex, C, 1, dz, dz);
 }
 
 // ECOS bring2cone: s = r + (1 + alpha) e
@@ -1541,6 +1550,17 @@ BMPC_HD void bring2cone(const X ex, const Ctx& C, const gdouble* r, gdouble* s) 
 template <class X>
 BMPC_HD double vdot(const X ex, const gdouble* a, const gdouble* b, int n) {
   return lane_sum(ex, 0, n, [&](int i) { return a[i] * b[i]; });
+}
+
+// a1'b1 (n1 entries) + a2'b2 (n2 entries) in one pass
+template <class X>
+BMPC_HD double dot2(const X ex, const gdouble* a1, const gdouble* b1, int n1, const gdouble* a2, const gdouble* b2,
+                    int n2) {
+  return lane_sum(ex, 0, n1 + n2, [&](int i) {
+    const bool f = i < n1;
+    const int j = f ? i : i - n1;
+    return (f ? a1 : a2)[j] * (f ? b1 : b2)[j];
+  });
 }
 
 struct IpmResult {
@@ -1630,28 +1650,42 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     // residuals
     apply_AT<X, NX, NU>(ex, C, y, rx);
     apply_GT<X, NX, NU>(ex, C, z, tA);
-    lane_batch<16>(ex, 0, nv, [&](int i) { return rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0)); }, [&](int i, double v) { rx[i] = v; });
+    // the norms and dot products are accumulated in the passes that produce rx, ry, rz
+    struct R2 { double v, a; };
+    struct R3 { double v, a, b; };
+    struct R5 { double v, a, b, c, d; };
+    double acx[2] = {0.0, 0.0}, acy[3] = {0.0, 0.0, 0.0}, acz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    lane_batch<8>(ex, 0, nv, [&](int i) {
+      const double xi = x[i];
+      return R2{rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0)), xi * xi};
+    }, [&](int i, R2 r) { rx[i] = r.v; acx[0] += r.v * r.v; acx[1] += r.a; });
     apply_A<X, NX, NU>(ex, C, x, ry);
-    lane_batch(ex, 0, neq, [&](int i) { return bv[i] * tau - ry[i]; }, [&](int i, double v) { ry[i] = v; });
+    lane_batch<8>(ex, 0, neq, [&](int i) {
+      const double yi = y[i], bi = bv[i];
+      return R3{bi * tau - ry[i], bi * yi, yi * yi};
+    }, [&](int i, R3 r) { ry[i] = r.v; acy[0] += r.v * r.v; acy[1] += r.a; acy[2] += r.b; });
     apply_G<X, NX, NU>(ex, C, x, rz);
-    lane_batch<16>(ex, 0, nr, [&](int i) { return hv[i] * tau - rz[i] - s[i]; }, [&](int i, double v) { rz[i] = v; });
+    lane_batch<4>(ex, 0, nr, [&](int i) {
+      const double zi = z[i], si = s[i], hi = hv[i];
+      return R5{hi * tau - rz[i] - si, hi * zi, zi * zi, si * si, si * zi};
+    }, [&](int i, R5 r) { rz[i] = r.v; acz[0] += r.v * r.v; acz[1] += r.a; acz[2] += r.b; acz[3] += r.c; acz[4] += r.d; });
     ex.sync();
     const double cx = x[P.oJ];
-    const double by = vdot(ex, bv, y, neq), hz = vdot(ex, hv, z, nr);
+    const double by = ex.sum(acy[1]), hz = ex.sum(acz[1]);
     const double rt = kap + cx + by + hz;
-    const double nx = sqrt(vdot(ex, x, x, nv)), ny = sqrt(vdot(ex, y, y, neq));
-    const double nz = sqrt(vdot(ex, z, z, nr)), ns = sqrt(vdot(ex, s, s, nr));
-    const double sz = vdot(ex, s, z, nr);
+    const double nx = sqrt(ex.sum(acx[1])), ny = sqrt(ex.sum(acy[2]));
+    const double nz = sqrt(ex.sum(acz[2])), ns = sqrt(ex.sum(acz[3]));
+    const double sz = ex.sum(acz[4]);
     const double mu = (sz + kap * tau) / (deg + 1.0);
     const double gap = sz / (tau * tau);
     const double pcost = cx / tau, dcost = -(hz + by) / tau;
     double relgap = -1.0;   // -1 = NaN
     if (pcost < 0.0) relgap = gap / (-pcost);
     else if (dcost > 0.0) relgap = gap / dcost;
-    const double nry = neq ? sqrt(vdot(ex, ry, ry, neq)) / fmax(resy0 + nx, 1.0) : 0.0;
-    const double nrz = sqrt(vdot(ex, rz, rz, nr)) / fmax(resz0 + nx + ns, 1.0);
+    const double nry = neq ? sqrt(ex.sum(acy[0])) / fmax(resy0 + nx, 1.0) : 0.0;
+    const double nrz = sqrt(ex.sum(acz[0])) / fmax(resz0 + nx + ns, 1.0);
     const double pres = fmax(nry, nrz) / tau;
-    const double dres = sqrt(vdot(ex, rx, rx, nv)) / fmax(resx0 + ny + nz, 1.0) / tau;
+    const double dres = sqrt(ex.sum(acx[0])) / fmax(resx0 + ny + nz, 1.0) / tau;
     BMPC_TOC(ws, L, PROF_RESID, t_res);
     // infeasibility certificates (only evaluated when their preconditions hold)
     double pinfres = -1.0, dinfres = -1.0;
@@ -1693,9 +1727,13 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i]; }, [&](int i, double v) { ws[L.bestx + i] = v; });
       ex.sync();
     }
-#ifdef BMPC_HOST_DEBUG
-    printf("it %3d pcost %+.9e dcost %+.9e gap %.2e pres %.2e dres %.2e k/t %.2e tau %.2e nx %.2e\n", it, pcost,
-           dcost, gap, pres, dres, kap / tau, tau, nx);
+#if defined(BMPC_HOST_DEBUG) || (defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__))
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (blockIdx.x == 0 && ex.lane == 0)
+#endif
+    printf("it %3d pcost %+.9e dcost %+.9e gap %.2e pres %.2e dres %.2e k/t %.2e tau %.2e nx %.2e ny %.2e nz %.2e ns %.2e"
+           " stall %d best %.3e maxit %d\n",
+           it, pcost, dcost, gap, pres, dres, kap / tau, tau, nx, ny, nz, ns, stall, best_score, P.desc.maxit);
 #endif
     int code = check(feastol, abstol, reltol);
     if (code == 99 && stall >= 5) {    // no progress for 5 end-game iterations: precision floor
@@ -1716,6 +1754,9 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       const int c2 = check(1e-4, 5e-5, 5e-5);
       code = c2 == 99 ? EXIT_MAXIT : c2 + EXIT_INACC;
     }
+#if defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__)
+    if (blockIdx.x == 0 && ex.lane == 0) printf("   code %d (it %d, stall %d)\n", code, it, stall);
+#endif
     if (code != 99) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] / tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
       ex.sync();
@@ -1736,21 +1777,18 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x1, y1, z1, nref);
-      const double den = kap / tau - (x1[P.oJ] + vdot(ex, bv, y1, neq) + vdot(ex, hv, z1, nr));
-      // affine: xi = -lam
-      lane_batch<16>(ex, 0, nr, [&](int i) { return -lam[i]; }, [&](int i, double v) { ra[i] = v; });
-      ex.sync();
-      apply_W(ex, C, 0, ra, rb);                               // W xi
-      lane_batch<16>(ex, 0, nr, [&](int i) { return rz[i] - rb[i]; }, [&](int i, double v) { rb[i] = v; });
+      const double den = kap / tau - (x1[P.oJ] + dot2(ex, bv, y1, neq, hv, z1, nr));
+      // affine: xi = -lam, rb = rz - W xi = rz + W lam
+      apply_W(ex, C, 0, lam, rb, 1.0, rz, 1.0);
       lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2, nref);
       const double dk_aff = -kap * tau;
-      const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
+      const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
       lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, dz, rb);                               // W dz_aff
-      lane_batch<16>(ex, 0, nr, [&](int i) { return ra[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff
+      lane_batch<16>(ex, 0, nr, [&](int i) { return -lam[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff = xi - W dz_aff
       ex.sync();
       const double dkap_a = (dk_aff - kap * dtau_a) / tau;
       double a_aff = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
@@ -1769,14 +1807,13 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;
       ex.sync();
       jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
-      apply_W(ex, C, 0, ds, rb);                               // W xi
-      lane_batch<16>(ex, 0, nr, [&](int i) { return eta1 * rz[i] - rb[i]; }, [&](int i, double v) { rb[i] = v; });
+      apply_W(ex, C, 0, ds, rb, -1.0, rz, eta1);               // eta1 rz - W xi
       lane_batch<16>(ex, 0, nv, [&](int i) { return -eta1 * rx[i]; }, [&](int i, double v) { tA[i] = v; });
       lane_batch(ex, 0, neq, [&](int i) { return eta1 * ry[i]; }, [&](int i, double v) { ya[i] = v; });
       ex.sync();
       kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2, nref);
       const double dk_c = -kap * tau - dtau_a * dkap_a + sigma * mu;
-      dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + vdot(ex, bv, y2, neq) + vdot(ex, hv, z2, nr)) / den;
+      dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
       lane_batch<16>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });
       lane_batch(ex, 0, neq, [&](int i) { return y2[i] + (dtau * y1[i]); }, [&](int i, double v) { y2[i] = v; });
       lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
