@@ -169,8 +169,9 @@ def main():
     sh = stream.cuda_stream
     env = abi.make_env()                       # main_branch.sim_overtake scene constants
     scene = torch.zeros((B, abi.ENV_STRIDE), device=dev, dtype=torch.float64)
-    scene[:, 0:4] = tx
-    scene[:, 4:8] = tz
+    if not quad:
+        scene[:, 0:4] = tx
+        scene[:, 4:8] = tz
     estats = torch.zeros((B, abi.ENV_NSTAT), device=dev, dtype=torch.float64)
     tstep = [0]
 
