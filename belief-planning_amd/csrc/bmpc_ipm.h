@@ -1415,7 +1415,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
 //   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
 template <class X, int NX, int NU>
-BMPC_FN void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
+BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
                             const gdouble* r3h, gdouble* dx, gdouble* dy, gdouble* dzh) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
