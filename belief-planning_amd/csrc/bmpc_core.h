@@ -136,7 +136,7 @@ struct Layout {
   // KKT-solve scratch
   size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_cx, k_cy, k_cz, k_nv1, zeros;
   // scaling
-  size_t dl, eta, wbar, vnt;
+  size_t dl, dli, eta, wbar, vnt;   // NT scaling: LP d and 1/d, cone eta, wbar, v
   // KKT
   size_t hx, hu, sd, P, Kg, Luu, kff, lvec, qx0, gk, colk, colnu;
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)

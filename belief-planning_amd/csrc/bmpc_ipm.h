@@ -526,8 +526,12 @@ BMPC_FN bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s, const 
   double bad = strided_partial<8, 1>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
     return (s[i] > 0.0 && z[i] > 0.0) ? 0.0 : 1.0;
   });
-  lane_batch(ex, 0, P.nlp, [&](int i) { return DL{sqrt(s[i] / z[i]), sqrt(s[i] * z[i])}; },
-             [&](int i, DL v) { dl[i] = v.d; lam[i] = v.l; });
+  gdouble* dli = C.at(C.L->dli);
+  struct DLI { double d, di, l; };
+  lane_batch(ex, 0, P.nlp, [&](int i) {
+    const double d = sqrt(s[i] / z[i]);
+    return DLI{d, 1.0 / d, sqrt(s[i] * z[i])};
+  }, [&](int i, DLI v) { dl[i] = v.d; dli[i] = v.di; lam[i] = v.l; });
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double sres = cone_res(ex, G, s, off, q);
@@ -567,7 +571,8 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   gdouble* dl = C.at(C.L->dl);
   gdouble* wb = C.at(C.L->wbar);
   gdouble* vn = C.at(C.L->vnt);
-  lane_batch(ex, 0, P.nlp, [&](int) { return 1.0; }, [&](int i, double v) { dl[i] = v; });
+  gdouble* dli = C.at(C.L->dli);
+  lane_batch(ex, 0, P.nlp, [&](int) { return 1.0; }, [&](int i, double v) { dl[i] = v; dli[i] = v; });
   const int c0 = P.nlp;
   lane_batch(ex, c0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { wb[i] = v; vn[i] = v; });
   ex.sync();
@@ -587,13 +592,13 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
                      const gdouble* add = nullptr, double sa = 0.0) {
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
-  const gdouble* dl = C.at(C.L->dl);
+  const gdouble* dl = C.at((mode == 0 || mode == 2) ? C.L->dl : C.L->dli);   // d or 1/d
   const gdouble* ad = add ? add : in;   // read and scaled by 0 without an addend
   if (!add) sa = 0.0;
+  const bool sq = mode >= 2;
   lane_batch<16>(ex, 0, P.nlp, [&](int i) {
     const double w = dl[i];
-    const double v = mode == 0 ? w * in[i] : mode == 1 ? in[i] / w : mode == 2 ? w * w * in[i] : in[i] / (w * w);
-    return sw * v + sa * ad[i];
+    return sw * ((sq ? w * w : w) * in[i]) + sa * ad[i];
   }, [&](int i, double v) { out[i] = v; });
   const gdouble* eta = C.at(C.L->eta);
   // W = e (2 v v' - J); W^-1 = (2 Jv Jv' - J)/e; W^2 = e^2 (2 wb wb' - J); W^-2 = (2 Jwb Jwb' - J)/e^2
@@ -718,7 +723,7 @@ BMPC_HD int branch_start(CPlan& P, int dep) {
 }
 
 // one Riccati step at a node with input: P = hx + A'Pb A - Qux' Quu^-1 Qux,
-// Quu = hu + B'Pb B (Cholesky stored), K = -Quu^-1 Qux (stored).  Pout receives P.
+// Quu = hu + B'Pb B (its inverse stored), K = -Quu^-1 Qux (stored).  Pout receives P.
 template <int NX, int NU>
 BMPC_HD bool riccati_step(const gdouble* hx, const gdouble* hu, const gdouble* Ap, const gdouble* Bp,
                           const double (&Pb)[NX][NX], double (&Pk)[NX][NX], gdouble* Luu_out, gdouble* K_out) {
@@ -770,7 +775,17 @@ BMPC_HD bool riccati_step(const gdouble* hx, const gdouble* hu, const gdouble* A
       Quu[i][j] += v;
     }
   const bool ok = chol<NU>(Quu);
-  mat_store(Quu, Luu_out);
+  double Qi[NU][NU];   // Quu^-1 (the tree sweeps multiply by it: no divisions on their chains)
+#pragma unroll
+  for (int j = 0; j < NU; ++j) {
+    double col[NU];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) col[i] = i == j ? 1.0 : 0.0;
+    chol_solve<NU>(Quu, col);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) Qi[i][j] = col[i];
+  }
+  mat_store(Qi, Luu_out);
   double K[NU][NX];
 #pragma unroll
   for (int j = 0; j < NX; ++j) {
@@ -987,8 +1002,12 @@ BMPC_HD void bw_node(const X& ex, int gl, const double (&qx)[RX], const double (
     qu[m] = -ru[m] + ex.tsum(v);
   }
 #pragma unroll
-  for (int m = 0; m < NU; ++m) kfv[m] = -qu[m];
-  chol_solve<NU>(Lu, kfv);
+  for (int m = 0; m < NU; ++m) {   // kf = -Quu^-1 qu  (Lu holds Quu^-1)
+    double v = 0.0;
+#pragma unroll
+    for (int c = 0; c < NU; ++c) v -= Lu[m][c] * qu[c];
+    kfv[m] = v;
+  }
 #pragma unroll
   for (int q = 0; q < RX; ++q) {
     double v = qx[q];
@@ -1442,19 +1461,36 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   const ldouble* bc = b + ng + nb;
   const gdouble* colk = ws + L.colk;
   const gdouble* colnu = ws + L.colnu;
-  auto woodbury_x = [&](int i) {
-    double v = dx[i];
-    for (int k = 0; k < nc; ++k) v -= bc[k] * colk[(size_t)k * P.nv + i];
-    return v;
+  // dx (tree and slack parts) and dy in one pass; the columns are loaded four at a time so a
+  // lane's loads are in flight together
+  const int n1 = P.oRho, n2 = n1 + (P.oJ - P.oS), n3 = n2 + P.T * NX;
+  auto row = [&](int t, int& i, bool& isx) {
+    isx = t < n2;
+    i = t < n1 ? t : t < n2 ? P.oS + (t - n1) : t - n2;
   };
-  auto put_x = [&](int i, double v) { dx[i] = v; };
-  lane_batch(ex, 0, P.oRho, woodbury_x, put_x);
-  lane_batch(ex, P.oS, P.oJ, woodbury_x, put_x);
-  lane_batch(ex, 0, P.T * NX, [&](int i) {
-    double v = dy[i];
-    for (int k = 0; k < nc; ++k) v -= bc[k] * colnu[(size_t)k * P.neq + i];
+  lane_batch(ex, 0, n3, [&](int t) {
+    int i;
+    bool isx;
+    row(t, i, isx);
+    const gdouble* col = isx ? colk : colnu;
+    const size_t cs = isx ? (size_t)P.nv : (size_t)P.neq;
+    double v = isx ? dx[i] : dy[i];
+    for (int k0 = 0; k0 < nc; k0 += 4) {
+      double c4[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) c4[a] = col[(size_t)(k0 + a < nc ? k0 + a : nc - 1) * cs + i];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        if (k0 + a < nc) v -= bc[k0 + a] * c4[a];
+    }
     return v;
-  }, [&](int i, double v) { dy[i] = v; });
+  }, [&](int t, double v) {
+    int i;
+    bool isx;
+    row(t, i, isx);
+    if (isx) dx[i] = v;
+    else dy[i] = v;
+  });
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) {
     if (i < ng) dx[gvar(P, i)] = b[i];
     else dy[P.T * NX + i - ng] = b[i];

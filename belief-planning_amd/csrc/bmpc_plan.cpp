@@ -395,6 +395,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.k_nv1 = take(nv);
   L.zeros = take(neq);   // all-zero eq-space vector (tree solves without an e term)
   L.dl = take(P.nlp);
+  L.dli = take(P.nlp);
   L.eta = take(nc);
   L.wbar = take(nr);
   L.vnt = take(nr);
