@@ -168,7 +168,7 @@ BMPC_FN void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out)
   struct Two { double a, b; };
   // branch-free bodies: every load of a batch is issued before the first wait (a branch on
   // a loaded topology index would serialise the batch into one round trip per element)
-  lane_batch(ex, 0, P.T * Nc, [&](int it) {
+  lane_batch<4>(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     const double S = zv[P.oS + it];
     const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
