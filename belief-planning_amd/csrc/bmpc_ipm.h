@@ -1821,10 +1821,10 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2, nref);
       const double dk_aff = -kap * tau;
       const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
-      lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
+      lane_batch<8>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, dz, rb);                               // W dz_aff
-      lane_batch<16>(ex, 0, nr, [&](int i) { return -lam[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff = xi - W dz_aff
+      lane_batch<8>(ex, 0, nr, [&](int i) { return -lam[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff = xi - W dz_aff
       ex.sync();
       const double dkap_a = (dk_aff - kap * dtau_a) / tau;
       double a_aff = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
@@ -1837,7 +1837,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       // combined: ds_comb = -lam o lam - dsW_a o Wdz_a + sigma mu e
       jprod(ex, C, lam, lam, ra);
       jprod(ex, C, ds, rb, rc);
-      lane_batch<16>(ex, 0, nr, [&](int i) { return -ra[i] - rc[i]; }, [&](int i, double v) { ra[i] = v; });
+      lane_batch<8>(ex, 0, nr, [&](int i) { return -ra[i] - rc[i]; }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
       lane_batch(ex, 0, P.nlp, [&](int i) { return ra[i] + (sigma * mu); }, [&](int i, double v) { ra[i] = v; });
       for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;
@@ -1850,12 +1850,12 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2, nref);
       const double dk_c = -kap * tau - dtau_a * dkap_a + sigma * mu;
       dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
-      lane_batch<16>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });
+      lane_batch<8>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });
       lane_batch(ex, 0, neq, [&](int i) { return y2[i] + (dtau * y1[i]); }, [&](int i, double v) { y2[i] = v; });
-      lane_batch<16>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
+      lane_batch<8>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
       ex.sync();
       apply_W(ex, C, 0, z2, rb);                               // W dz
-      lane_batch<16>(ex, 0, nr, [&](int i) { return ds[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW
+      lane_batch<8>(ex, 0, nr, [&](int i) { return ds[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW
       ex.sync();
       dkap = (dk_c - kap * dtau) / tau;
       double a = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
@@ -1869,10 +1869,10 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       fin = ex.max(fin);
       ok = fin == 0.0 && isfinite(dtau) && alpha > 1e-10;
       if (ok) {
-        lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
+        lane_batch<8>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
         lane_batch(ex, 0, neq, [&](int i) { return y[i] + (alpha * y2[i]); }, [&](int i, double v) { y[i] = v; });
         struct ZS { double z, s; };
-        lane_batch<16>(ex, 0, nr, [&](int i) { return ZS{z[i] + alpha * z2[i], s[i] + alpha * rb[i]}; },
+        lane_batch<4>(ex, 0, nr, [&](int i) { return ZS{z[i] + alpha * z2[i], s[i] + alpha * rb[i]}; },
                    [&](int i, ZS v) { z[i] = v.z; s[i] = v.s; });
         tau += alpha * dtau;
         kap += alpha * dkap;
