@@ -35,6 +35,23 @@
 #define BMPC_REFTOL 1e-14    // refinement stop: scaled residual <= tol * max(1, |rhs|) (oracle: 1e-14)
 #endif
 
+// per-phase inlining overrides (experiments: -DBMPC_FN_APPLY_G=BMPC_HD ...)
+#ifndef BMPC_FN_APPLY_G
+#define BMPC_FN_APPLY_G BMPC_FN
+#endif
+#ifndef BMPC_FN_APPLY_GT
+#define BMPC_FN_APPLY_GT BMPC_FN
+#endif
+#ifndef BMPC_FN_SCALING
+#define BMPC_FN_SCALING BMPC_FN
+#endif
+#ifndef BMPC_FN_MAX_STEP
+#define BMPC_FN_MAX_STEP BMPC_FN
+#endif
+#ifndef BMPC_FN_TREE_SOLVE
+#define BMPC_FN_TREE_SOLVE BMPC_FN
+#endif
+
 namespace bmpc {
 
 enum {
@@ -153,7 +170,7 @@ BMPC_HD double fx_coef(const Ctx& C, int k, int c, int j) {
 
 // out(rows) = G zv, cone rows boosted
 template <class X, int NX, int NU>
-BMPC_FN void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out) {
+BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out) {
   const Ctx C = Cin.uniform();
   double qx[NX];
   ctx_qx<NX>(C, qx);
@@ -264,7 +281,7 @@ BMPC_FN void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out)
 
 // out(nv) = G' r (+ add, when add is not NULL)
 template <class X, int NX, int NU>
-BMPC_FN void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out, const gdouble* add = nullptr) {
+BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdouble* out, const gdouble* add = nullptr) {
   const Ctx C = Cin.uniform();
   add = uniform_ptr(add);
   const double sa = add ? 1.0 : 0.0;
@@ -513,7 +530,7 @@ BMPC_HD void build_hb(const X ex, const Ctx& C, gdouble* h, gdouble* bv) {
 // ------------------------------------------------------------------------------------
 // returns false when an iterate left its cone
 template <class X>
-BMPC_FN bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s, const gdouble* z) {
+BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s, const gdouble* z) {
   const Ctx C = Cin.uniform();
   BMPC_PROF(C.ws, *C.L, PROF_SCALING);
   CPlan& P = *C.P;
@@ -682,7 +699,7 @@ BMPC_HD void jdiv(const X ex, const Ctx& C, const gdouble* lam, const gdouble* v
 
 // largest alpha with lam + alpha d in the cone (ECOS lineSearch for one direction)
 template <class X>
-BMPC_FN double max_step(const X ex, const Ctx Cin, const gdouble* lam, const gdouble* d) {
+BMPC_FN_MAX_STEP double max_step(const X ex, const Ctx Cin, const gdouble* lam, const gdouble* d) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
@@ -1030,7 +1047,7 @@ BMPC_HD void bw_node(const X& ex, int gl, const double (&qx)[RX], const double (
 // the affine term l / the state x in registers along the branch -- only the Riccati data
 // is loaded per node; (3) lane-parallel post-pass: multipliers nu and slack recovery.
 template <class X, int NX, int NU>
-BMPC_FN void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* r0, size_t rs, const gdouble* e0,
+BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* r0, size_t rs, const gdouble* e0,
                         size_t es, gdouble* o0, size_t os, gdouble* n0, size_t ns) {
   const Ctx C = Cin.uniform();
   r0 = uniform_ptr(r0);
