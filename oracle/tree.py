@@ -694,3 +694,173 @@ class BranchQPController(ProxController):
                            self.Qslack[0] * sp.eye(nS)], format='csc')
         qv = np.concatenate([qx, qu, self.Qslack[1] * self.slackweight])
         return 2.0 * H, qv
+
+
+# ---------------------------------------------------------------------------------------
+# robustMPC
+# ---------------------------------------------------------------------------------------
+class RobustController:
+    """Oracle restatement of ``robustMPC`` (MPC_branch.py:1275-1595).
+
+    One input sequence over a chain of Nx = N*NB + 2 states / Nu = N*NB + 1 inputs must clear
+    every obstacle prediction of the scenario tree: at time slot t (0 <= t <= N*NB) there is
+    one collision row per prediction of the obstacle at t -- the measured z at t = 0, then
+    m**depth rows (BFS order of the branches, ``inittree`` :1336-1360).  Every state row gets
+    a slack (``buildIneqConstr`` :1467-1510); the cost is unweighted (``buildCost``
+    :1540-1569).  The linearisation trajectory is the previous prediction shifted by one
+    step (``solve`` :1429-1431); the first solve rolls out u = 0 from x (``get_xLin`` :1326).
+    The branch probabilities the reference computes on an uninitialised root trajectory
+    (:1337, :1353) only feed branch weights that nothing reads, so they are not restated."""
+
+    def __init__(self, model, N, NB, Q, R, dR, Fx, bx, Fu, bu, Qslack, xRef, Qf=None, solver=None):
+        self.model = model
+        self.n, self.d, self.m = model.n, model.d, model.m
+        self.N, self.NB = N, NB
+        self.Nx, self.Nu = N * NB + 2, N * NB + 1
+        self.Q, self.R = np.asarray(Q, float), np.asarray(R, float)
+        self.Qf = self.Q if Qf is None else np.asarray(Qf, float)
+        self.dR = np.asarray(dR, float)
+        self.Fx = np.asarray(Fx, float).reshape(-1, self.n)
+        self.bx = np.asarray(bx, float).reshape(-1)
+        self.Fu = np.asarray(Fu, float)
+        self.bu = np.asarray(bu, float).reshape(-1)
+        self.Qslack = np.asarray(Qslack, float)
+        self.xRef = np.asarray(xRef, float)
+        self.xLin = self.uLin = None
+        self.xPred = self.uPred = None
+        self.OldInput = np.zeros(self.d)
+        self.feasible = 0
+        self.solver = solver
+        self.last_problem = None
+        self.zPred = None
+        self.ztraj = None
+
+    def predictions(self, z):
+        """Obstacle predictions per time slot (``inittree`` / ``updatetree``) and the BFS
+        branch trajectories that ``BT2array`` returns (parent's last z prepended)."""
+        n, m, N = self.n, self.m, self.N
+        zPred = [np.zeros((0, n)) for _ in range(self.N * self.NB + 1)]
+        zPred[0] = np.array([z])
+        ztraj = []
+        q = [(0, np.reshape(z, (1, n)))]
+        while q:
+            depth, zt = q.pop(0)
+            if depth > 0:
+                for i in range(zt.shape[0]):
+                    t = (depth - 1) * N + i + 1
+                    zPred[t] = np.vstack((zPred[t], zt[i]))
+            if depth < self.NB:
+                zp = self.model.zpred_eval(zt[-1])
+                for i in range(m):
+                    child = zp[:, n * i:n * (i + 1)]
+                    ztraj.append(np.vstack((zt[-1], child)))
+                    q.append((depth + 1, child))
+        return zPred, ztraj
+
+    def linearisation(self, x):
+        """``get_xLin`` on the first solve, then the carried shifted prediction; the dynamics
+        of every input node (``computeLTVdynamics`` :1438-1443)."""
+        if self.xLin is None:
+            self.uLin = np.vstack((np.zeros((self.Nu, self.d)), np.zeros((1, self.d))))
+            self.xLin = np.zeros((self.Nx, self.n))
+            self.xLin[0] = x
+            for i in range(self.Nx - 1):
+                self.xLin[i + 1] = self.model.dyn_linearization(self.xLin[i], self.uLin[i])[3]
+        return [self.model.dyn_linearization(self.xLin[i], self.uLin[i])[:3] for i in range(self.Nu)]
+
+    def setup_problem(self, x, z, xRef=None):
+        x = np.asarray(x, float)
+        z = np.asarray(z, float)
+        if xRef is not None:
+            self.xRef = np.asarray(xRef, float)
+        n, d, Nx, Nu = self.n, self.d, self.Nx, self.Nu
+        self.zPred, self.ztraj = self.predictions(z)
+        dyn = self.linearisation(x)
+        nFx, nFu = self.Fx.shape[0], self.Fu.shape[0]
+        # inequalities: [Fx rows of every node | collision rows | Fu rows | -S <= 0]
+        colrows = []
+        for i, zs in enumerate(self.zPred):
+            for j in range(zs.shape[0]):
+                h, dh = self.model.col_eval(self.xLin[i], zs[j])
+                colrows.append((i, -np.asarray(dh, float), float(h)))
+        nS = Nx * nFx + len(colrows)
+        nX, nU = Nx * n, Nu * d
+        rows, cols, vals = [], [], []
+        for k in range(Nx):
+            for r in range(nFx):
+                for c in range(n):
+                    if self.Fx[r, c] != 0.0:
+                        rows.append(k * nFx + r); cols.append(k * n + c); vals.append(self.Fx[r, c])
+        r0 = Nx * nFx
+        for e, (i, a, _) in enumerate(colrows):
+            for c in range(n):
+                if a[c] != 0.0:
+                    rows.append(r0 + e); cols.append(i * n + c); vals.append(a[c])
+        for k in range(nS):
+            rows.append(k); cols.append(nX + nU + k); vals.append(-1.0)
+        r0 = nS
+        for u in range(Nu):
+            for r in range(nFu):
+                for c in range(d):
+                    if self.Fu[r, c] != 0.0:
+                        rows.append(r0 + u * nFu + r); cols.append(nX + u * d + c); vals.append(self.Fu[r, c])
+        r0 += Nu * nFu
+        for k in range(nS):
+            rows.append(r0 + k); cols.append(nX + nU + k); vals.append(-1.0)
+        r0 += nS
+        F = _coo(rows, cols, vals, (r0, nX + nU + nS))
+        bineq = np.concatenate([np.tile(self.bx, Nx), [h for _, _, h in colrows], np.tile(self.bu, Nu), np.zeros(nS)])
+        # equalities: x_0 = x, x_{i+1} - A_i x_i - B_i u_i = C_i
+        rows, cols, vals = list(range(nX)), list(range(nX)), [1.0] * nX
+        beq = np.zeros(nX)
+        beq[:n] = x
+        for i, (A, B, C) in enumerate(dyn):
+            for r in range(n):
+                for c in range(n):
+                    if A[r, c] != 0.0:
+                        rows.append((i + 1) * n + r); cols.append(i * n + c); vals.append(-A[r, c])
+                for c in range(d):
+                    if B[r, c] != 0.0:
+                        rows.append((i + 1) * n + r); cols.append(nX + i * d + c); vals.append(-B[r, c])
+            beq[(i + 1) * n:(i + 2) * n] = C
+        G = _coo(rows, cols, vals, (nX, nX + nU + nS))
+        # cost: 2 blockdiag(Q .. Q, Qf, Hu, Qs0 I); Hu = R + 2 dR (last block R + dR), -dR couplings
+        dRm = np.diag(self.dR)
+        Hu = np.zeros((nU, nU))
+        for u in range(Nu):
+            Hu[u * d:(u + 1) * d, u * d:(u + 1) * d] = self.R + (2 * dRm if u < Nu - 1 else dRm)
+            if u + 1 < Nu:
+                Hu[(u + 1) * d:(u + 2) * d, u * d:(u + 1) * d] = -dRm
+                Hu[u * d:(u + 1) * d, (u + 1) * d:(u + 2) * d] = -dRm
+        H = sp.block_diag([sp.block_diag([self.Q] * (Nx - 1) + [self.Qf]), sp.csc_matrix(Hu),
+                           self.Qslack[0] * sp.eye(nS)], format='csc')
+        qx = np.concatenate([-2 * (self.xRef @ self.Q)] * (Nx - 1) + [-2 * (self.xRef @ self.Qf)])
+        qu = np.zeros(nU)
+        qu[:d] = -2 * (np.reshape(self.OldInput, -1) * self.dR)
+        qv = np.concatenate([qx, qu, self.Qslack[1] * np.ones(nS)])
+        A = sp.vstack([F, G]).tocsc()
+        lo = np.concatenate([-np.inf * np.ones(len(bineq)), beq])
+        hi = np.concatenate([bineq, beq])
+        self.last_problem = QPProblem((2.0 * H).tocsc(), qv, A, lo, hi, len(bineq))
+        return self.last_problem
+
+    def solve(self, x, z, xRef=None):
+        prob = self.setup_problem(x, z, xRef)
+        sol, info = self.solver(prob)
+        self.last_info = info
+        self.accept(sol, info['status_val'])
+
+    def accept(self, sol, status_val):
+        """``osqp_solve_qp`` (:1591-1595), ``unpackSolution`` (:1459-1465) -- the solution is
+        taken whatever the status -- then the time-varying shift (:1429-1434)."""
+        n, d = self.n, self.d
+        self.feasible = 1 if status_val == 1 else 0
+        self.Solution = sol
+        self.xPred = sol[:self.Nx * n].reshape(self.Nx, n).copy()
+        self.uPred = sol[self.Nx * n:self.Nx * n + self.Nu * d].reshape(self.Nu, d).copy()
+        self.xLin = np.vstack((self.xPred[1:], self.xPred[-1]))
+        self.uLin = np.vstack((self.uPred[1:], self.uPred[-1]))
+        self.OldInput = self.uPred[0, :].copy()
+
+    def BT2array(self):
+        return [self.xPred], self.ztraj, [self.uPred], []

@@ -140,3 +140,41 @@ def test_branch_qp_assembly_matches_reference():
             _inject_ws(c, g, t)
         prob = c.setup_problem(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t])
         _check_qp(prob, g, t, "branch-qp")
+
+
+def _robust(g, t):
+    from oracle.qp_ipm import osqp_like_solve
+    from oracle.tree import RobustController
+    mdl = HighwayModel(int(g["N"]), float(g["dt"]), highway_policies(float(g["Kpsi"]), g["traj_lc_target"][t]),
+                       L=float(g["L"]), W=float(g["W"]), s1=float(g["s1"]))
+    return RobustController(mdl, int(g["N"]), int(g["NB"]), g["Q"], g["R"], g["dR"], g["Fx"], g["bx"], g["Fu"],
+                            g["bu"], g["Qslack"], g["xRef0"], Qf=g["Qf"], solver=osqp_like_solve)
+
+
+@pytest.mark.parametrize("name", ["highway_robust_n20_nb1", "highway_robust_n8_nb2"])
+def test_robust_assembly_matches_reference(name):
+    """robustMPC (MPC_branch.py:1275): the reference's OSQP problem rebuilt by the oracle from
+    the warm start it carried (shifted prediction, OldInput), and its obstacle tree."""
+    g = golden(name)
+    for t in (int(k) for k in g["keep"]):
+        c = _robust(g, t)
+        if t > 0:
+            c.xLin = g["traj_ws_xLin"][t].copy()
+            c.uLin = g["traj_ws_uLin"][t].copy()
+            c.OldInput = g["traj_ws_old"][t].copy()
+        prob = c.setup_problem(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t])
+        _check_qp(prob, g, t, name)
+        np.testing.assert_allclose(np.array(c.ztraj), g[f"s{t}_bt_z"], rtol=0, atol=1e-12)
+
+
+def test_robust_closed_loop_replay():
+    """The oracle robustMPC driven through the recorded loop: its warm start after each step
+    equals the reference's (shifted prediction to 1e-7, the OSQP stand-in's tolerance)."""
+    g = golden("highway_robust_n8_nb2")
+    c = _robust(g, 0)
+    for t in range(6):
+        c.model.update_backup(highway_policies(float(g["Kpsi"]), g["traj_lc_target"][t]))
+        c.solve(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t])
+        np.testing.assert_allclose(c.uPred, g["traj_uPred"][t], atol=1e-7)
+        np.testing.assert_allclose(c.xPred, g["traj_xPred"][t], atol=1e-7)
+        assert c.feasible == 1 and g["traj_status"][t] == 1

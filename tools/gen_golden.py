@@ -242,6 +242,63 @@ def gen_highway_qp(name, N, NB, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+def gen_highway_robust(name, N, NB, steps, keep, out):
+    """The overtake scene with ``robustMPC`` (MPC_branch.py:1275-1595): one input sequence
+    that must clear every obstacle prediction of the scenario tree."""
+    import Init_MPC
+    import MPC_branch
+    from utils import Branch_constants
+
+    n, d, dt, am, rm, N_lane = 4, 2, 0.1, 6.0, 0.3, 4
+    xRef0 = np.array([0.5, 1.8, 15, 0])
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
+                            s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
+    mpc = MPC_branch.robustMPC(param, model)
+    CURRENT["mpc"] = mpc
+    env = HighwayOvertake(mpc, model, N_lane=N_lane, L=cons.L, W=cons.W, Kpsi=cons.Kpsi,
+                          lc_target0=xRef0, dt=dt)
+    d_out = dict(N=N, NB=NB, m=3, n=n, d=d, dt=dt, am=am, rm=rm, N_lane=N_lane,
+                 L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef0,
+                 Q=param.Q, Qf=param.Qf, R=param.R, dR=param.dR, Fx=param.Fx,
+                 bx=np.asarray(param.bx, float).reshape(-1),
+                 Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "status", "collision",
+                            "ws_xLin", "ws_uLin", "ws_old", "xPred", "uPred")}
+    Nx, Nu = N * NB + 2, N * NB + 1
+    for t in range(steps):
+        if not env.collision:
+            env.check_collision()
+        # warm start carried into this solve: the shifted previous prediction
+        # (MPC_branch.py:1429-1431) and the rate-cost OldInput (:1434)
+        first = mpc.BT is None
+        traj["ws_xLin"].append(np.full((Nx, n), np.nan) if first else np.array(mpc.xLin, float).copy())
+        traj["ws_uLin"].append(np.full((Nu, d), np.nan) if first else np.array(mpc.uLin, float).copy())
+        traj["ws_old"].append(np.array(mpc.OldInput, float).reshape(-1).copy())
+        r = env.step(t)
+        prob, sol, info, kw = CURRENT["captured"]
+        assert kw == {"verbose": False, "polish": True}, kw
+        for k in ("x", "z", "xRef", "u", "lc_target"):
+            traj[k].append(r[k])
+        traj["status"].append(info["status_val"])
+        traj["collision"].append(env.collision)
+        traj["xPred"].append(np.array(mpc.xPred, float))
+        traj["uPred"].append(np.array(mpc.uPred, float))
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.P, p + "P", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "q"], d_out[p + "l"], d_out[p + "u"] = prob.q, prob.l, prob.u
+            d_out[p + "sol"] = sol
+            d_out[p + "bt_z"] = np.array(mpc.BT2array()[1])
+        print(f"[{name}] t={t:3d} status={info['status_val']} it={info['iter']} u0={mpc.uPred[0]}", flush=True)
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def gen_quadruped(name, steps, keep, out):
     import Init_MPC
     import MPC_branch
@@ -328,6 +385,8 @@ def main():
         "highway_n10_nb1": lambda: gen_highway("highway_n10_nb1", 10, 1, 5 if a.quick else 20, {0, 1}, out),
         "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 2, {0, 1}, out),
         "highway_qp_n8_nb2": lambda: gen_highway_qp("highway_qp_n8_nb2", 8, 2, 5 if a.quick else 30, {0, 1, 2, 15}, out),
+        "highway_robust_n20_nb1": lambda: gen_highway_robust("highway_robust_n20_nb1", 20, 1, 5 if a.quick else 30, {0, 1, 2, 15}, out),
+        "highway_robust_n8_nb2": lambda: gen_highway_robust("highway_robust_n8_nb2", 8, 2, 5 if a.quick else 20, {0, 1, 10}, out),
         "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
     }
     for k, f in jobs.items():
