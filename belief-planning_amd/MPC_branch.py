@@ -238,14 +238,6 @@ class BranchMPC_CVaR:
         return self._tree_arrays()["sol"]
 
 
-class _NotBuilt:
-    _what = ""
-
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError(f"{self._what} is not built in this version of the MI355X library "
-                                  "(see DESIGN.md, scope)")
-
-
 class BranchMPCProx(BranchMPC_CVaR):
     """Proximal branch QP (MPC_branch.py:82-488) on MI355X: the OSQP problem of
     buildCost/buildEqConstr/buildIneqConstr solved by the device QP interior point.
@@ -274,6 +266,47 @@ class BranchMPC(BranchMPCProx):
     controller_kind = abi.CTRL_QP
 
 
-class robustMPC(_NotBuilt):
-    """Robust branch QP (MPC_branch.py:1275-1595)."""
-    _what = "robustMPC"
+class robustMPC(BranchMPCProx):
+    """Robust MPC (MPC_branch.py:1275-1595) on MI355X: one input sequence over a chain of
+    Nx = N*NB+2 states / Nu = N*NB+1 inputs that must clear every obstacle prediction of the
+    scenario tree, solved by the device QP interior point (controller kind ROBUST).  The
+    solution is taken whatever the OSQP status (unpackSolution :1459); the next solve
+    linearises about the prediction shifted by one step (:1429-1431); OldInput = uPred[0]."""
+
+    controller_kind = abi.CTRL_ROBUST
+
+    def __init__(self, mpcParameters, predictiveModel, batch=1, device=0):
+        super().__init__(mpcParameters, predictiveModel, batch=batch, device=device)
+        self.Nx, self.Nu = self.N * self.NB + 2, self.N * self.NB + 1
+        self.totalx, self.totalu, self.branchdim = self.Nx, self.Nu, 0
+        self.slackdim = None
+        self._z = None
+
+    def solve(self, x, z, xRef=None):
+        """One controller step (MPC_branch.py:1397-1435)."""
+        self._z = np.asarray(z, float).copy()
+        super().solve(x, z, xRef)
+
+    def _unpack(self, r, e):
+        super()._unpack(r, e)
+        self.xLin = np.vstack((self.xPred[1:], self.xPred[-1]))
+        self.uLin = np.vstack((self.uPred[1:], self.uPred[-1]))
+        self.zt, self.zt_u = self.xPred[-1, :], self.uPred[-1, :]
+
+    def BT2array(self, e=0):
+        """([xPred], ztraj, [uPred], []) with ztraj the obstacle branches in BFS order, each
+        prefixed by its parent's last prediction (:1385-1396)."""
+        n, m = self.n, self.m
+        ztraj, q = [], [(0, np.reshape(self._z, (1, n)))]
+        while q:
+            depth, zt = q.pop(0)
+            if depth < self.NB:
+                zp = self.predictiveModel.zpred_eval(zt[-1])
+                for i in range(m):
+                    child = zp[:, n * i:n * (i + 1)]
+                    ztraj.append(np.vstack((zt[-1], child)))
+                    q.append((depth + 1, child))
+        return [self.xPred], ztraj, [self.uPred], []
+
+    def build_tree(self, e=0):
+        raise NotImplementedError("robustMPC keeps no branch tree of states (MPC_branch.py:1336)")

@@ -69,6 +69,8 @@ _SIGS = {
     "bmpc_get_warm_start": (C.c_int, [C.c_void_p] * 4),
     "bmpc_get_counters": (C.c_int, [C.c_void_p] * 2),
     "bmpc_set_warm_start": (C.c_int, [C.c_void_p] * 5),
+    "bmpc_get_robust_warm_start": (C.c_int, [C.c_void_p] * 4),
+    "bmpc_set_robust_warm_start": (C.c_int, [C.c_void_p] * 5),
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),

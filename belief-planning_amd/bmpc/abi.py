@@ -7,7 +7,7 @@ import numpy as np
 
 MAX_N, MAX_D, MAX_FX, MAX_FU, MAX_M = 8, 4, 8, 8, 4
 
-CTRL_CVAR, CTRL_PROX, CTRL_QP = 0, 1, 2
+CTRL_CVAR, CTRL_PROX, CTRL_QP, CTRL_ROBUST = 0, 1, 2, 3
 MODEL_HIGHWAY, MODEL_QUADRUPED = 0, 1
 POL_MAINTAIN, POL_BRAKE, POL_LC, POL_MAINTAIN_TRACKV, POL_FORWARD, POL_STOP = range(6)
 

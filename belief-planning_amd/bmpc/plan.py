@@ -115,6 +115,23 @@ class BatchPlan:
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         check(lib().bmpc_set_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(old), _p(m)), "bmpc_set_warm_start")
 
+    def get_robust_warm_start(self):
+        """robustMPC's warm start: xLin [B,T,n], uLin [B,U,d], OldInput [B,d]."""
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        xl, ul, old = np.zeros((B, self.T, n)), np.zeros((B, self.U, d)), np.zeros((B, d))
+        check(lib().bmpc_get_robust_warm_start(self._h, _p(xl), _p(ul), _p(old)), "bmpc_get_robust_warm_start")
+        return dict(xLin=xl, uLin=ul, old_input=old)
+
+    def set_robust_warm_start(self, xLin, uLin, old_input=None, mask=None):
+        """robustMPC resume: the shifted prediction (MPC_branch.py:1429-1431) and OldInput."""
+        B, n, d = self.batch, self.desc.n, self.desc.d
+        xl = np.ascontiguousarray(np.asarray(xLin, np.float64).reshape(B, self.T, n))
+        ul = np.ascontiguousarray(np.asarray(uLin, np.float64).reshape(B, self.U, d))
+        old = None if old_input is None else np.ascontiguousarray(np.asarray(old_input, np.float64).reshape(B, d))
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_set_robust_warm_start(self._h, _p(xl), _p(ul), _p(old), _p(m)),
+              "bmpc_set_robust_warm_start")
+
     def tree(self):
         B, n, d = self.batch, self.desc.n, self.desc.d
         out = dict(xbar=np.zeros((B, self.T, n)), ubar=np.zeros((B, self.U, d)),

@@ -102,6 +102,10 @@ struct Topo {
 struct Plan {
   bmpc_plan_desc desc;
   int n, d, N, NB, m, nFx, nFu, Nc;
+  // collision rows per state node (robustMPC: one per obstacle prediction of the node's time
+  // slot, padded to m^NB; the others 1) and the obstacle tree depth (robustMPC's QP is a
+  // chain, NB = 0, over a scenario tree of obstacle predictions of depth zNB)
+  int Ncol, zNB;
   int T, U, nbranch, bdim, ncones, nlevels;
   // primal vector layout (reference sol['x'] layout, MPC_branch.py:2100-2102)
   int oX, oU, oRho, oSig, oMup, oMum, oS, oJ, nv;
@@ -142,6 +146,8 @@ struct Layout {
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
   // BranchMPCProx QP: u-rate couplings, linear cost, augmented Riccati P~, [Kx Kv], l~
   size_t qo, qq, Pa, Ka, la;
+  // robustMPC: carried linearisation trajectory, obstacle predictions [time][Ncol][n]
+  size_t xlin, zrob;
   size_t stride;  // doubles per ego
 };
 
@@ -149,7 +155,7 @@ typedef const BMPC_AS_CONST Plan CPlan;
 typedef const BMPC_AS_CONST Layout CLayout;
 
 // misc slots
-enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */ };
+enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */, MISC_X0 = 8 /* n values (robustMPC) */ };
 
 // ------------------------------------------------------------------------------------
 // phase cycle counters: built with -DBMPC_PROFILE the device code accumulates s_memtime

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, doubl
   DevExec ex{(int)threadIdx.x, nullptr};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   BMPC_PROF(E.ws, L, PROF_TREE);
-  tree_update<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+  tree_step<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
 }
 
 template <class M>
@@ -553,6 +553,53 @@ int bmpc_set_warm_start(bmpc_plan* pl, const double* uLin, const double* p, cons
   const Part parts[] = {{uLin, L.uLin, (P.U + 1) * P.d},
                         {p, L.pprev, P.bdim * P.m},
                         {jcons, L.misc + MISC_JCONS, 1},
+                        {old_input, L.misc + MISC_OLDU, P.d},
+                        {ones.data(), L.misc + MISC_INIT, 1}};
+  for (const Part& pt : parts) {
+    if (!pt.src || pt.cnt <= 0) continue;
+    double* buf = nullptr;
+    HIPCHECK(hipMalloc(&buf, sizeof(double) * (size_t)B * pt.cnt));
+    HIPCHECK(hipMemcpy(buf, pt.src, sizeof(double) * (size_t)B * pt.cnt, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, pt.off, pt.cnt, buf,
+                       dmask, B);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(pl->stream));
+    hipFree(buf);
+  }
+  if (dmask) hipFree(dmask);
+  return 0;
+}
+
+int bmpc_get_robust_warm_start(bmpc_plan* pl, double* xLin, double* uLin, double* old_input) {
+  if (!pl) return fail(-22, "null argument");
+  if (pl->hp.plan.desc.controller != BMPC_CTRL_ROBUST) return fail(-22, "not a robustMPC plan");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  int rc;
+  if (xLin && (rc = gather(pl, L.xlin, P.T * P.n, xLin))) return rc;
+  if (uLin && (rc = gather(pl, L.uLin, P.U * P.d, uLin))) return rc;
+  if (old_input && (rc = gather(pl, L.misc + MISC_OLDU, P.d, old_input))) return rc;
+  return 0;
+}
+
+int bmpc_set_robust_warm_start(bmpc_plan* pl, const double* xLin, const double* uLin, const double* old_input,
+                               const uint8_t* mask) {
+  if (!pl) return fail(-22, "null argument");
+  if (pl->hp.plan.desc.controller != BMPC_CTRL_ROBUST) return fail(-22, "not a robustMPC plan");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  const Layout& L = pl->hp.lay;
+  const int B = pl->batch;
+  uint8_t* dmask = nullptr;
+  if (mask) {
+    HIPCHECK(hipMalloc(&dmask, B));
+    HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
+  }
+  std::vector<double> ones(B, 1.0);
+  struct Part { const double* src; size_t off; int cnt; };
+  const Part parts[] = {{xLin, L.xlin, P.T * P.n},
+                        {uLin, L.uLin, P.U * P.d},
                         {old_input, L.misc + MISC_OLDU, P.d},
                         {ones.data(), L.misc + MISC_INIT, 1}};
   for (const Part& pt : parts) {

@@ -99,8 +99,10 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   memset(&P, 0, sizeof(P));
   P.desc = desc;
   const int n = desc.n, d = desc.d, N = desc.N, NB = desc.NB, m = desc.m;
-  if (desc.controller != BMPC_CTRL_CVAR && desc.controller != BMPC_CTRL_PROX && desc.controller != BMPC_CTRL_QP)
+  if (desc.controller != BMPC_CTRL_CVAR && desc.controller != BMPC_CTRL_PROX && desc.controller != BMPC_CTRL_QP &&
+      desc.controller != BMPC_CTRL_ROBUST)
     return "unknown controller";
+  const bool robust = desc.controller == BMPC_CTRL_ROBUST;
   if (desc.model == BMPC_MODEL_HIGHWAY) {
     if (n != 4 || d != 2) return "highway model needs n=4, d=2";
   } else if (desc.model == BMPC_MODEL_QUADRUPED) {
@@ -112,8 +114,16 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   if (desc.nFx < 0 || desc.nFx > BMPC_MAX_FX || desc.nFu < 0 || desc.nFu > BMPC_MAX_FU)
     return "too many constraint rows";
   if (!(desc.dt > 0.0)) return "dt must be positive";
-  P.n = n, P.d = d, P.N = N, P.NB = NB, P.m = m, P.nFx = desc.nFx, P.nFu = desc.nFu;
-  P.Nc = desc.nFx + 1;
+  // robustMPC: the QP is a chain (one leaf root branch of N*NB+1 nodes + terminal node); the
+  // scenario tree only shapes the obstacle predictions (MPC_branch.py:1301-1302,1336-1360)
+  const int NBt = robust ? 0 : NB;
+  P.n = n, P.d = d, P.N = N, P.NB = NBt, P.m = m, P.nFx = desc.nFx, P.nFu = desc.nFu;
+  P.zNB = NB;
+  P.Ncol = 1;
+  if (robust)
+    for (int k = 0; k < NB; ++k) P.Ncol *= m;
+  if (P.Ncol > 64) return "too many obstacle predictions (m^NB > 64)";
+  P.Nc = desc.nFx + P.Ncol;
   if (P.desc.maxit <= 0) P.desc.maxit = 100;
   if (!(P.desc.feastol > 0)) P.desc.feastol = 1e-8;
   if (!(P.desc.abstol > 0)) P.desc.abstol = 1e-8;
@@ -121,17 +131,17 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
 
   // ---- BFS topology (MPC_branch.inittree :1678-1747) ----------------------------------
   hp.br_depth = {0};
-  hp.br_len = {1};
+  hp.br_len = {robust ? N * NB + 1 : 1};
   hp.br_parent = {-1};
   hp.br_ndx = {0};
   hp.br_ndu = {0};
   hp.br_child0 = {-1};
-  int cx = 1, cu = 1;
+  int cx = hp.br_len[0] + (NBt == 0 ? 1 : 0), cu = hp.br_len[0];   // root nodes (+ terminal if a leaf)
   std::deque<int> q{0};
   while (!q.empty()) {
     const int b = q.front();
     q.pop_front();
-    if (hp.br_depth[b] >= NB) continue;
+    if (hp.br_depth[b] >= NBt) continue;
     hp.br_child0[b] = (int)hp.br_depth.size();
     for (int i = 0; i < m; ++i) {
       const int c = (int)hp.br_depth.size();
@@ -141,7 +151,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
       hp.br_child0.push_back(-1);
       hp.br_ndx.push_back(cx);
       hp.br_ndu.push_back(cu);
-      cx += hp.br_depth[c] == NB ? N + 1 : N;
+      cx += hp.br_depth[c] == NBt ? N + 1 : N;
       cu += N;
       q.push_back(c);
     }
@@ -149,10 +159,10 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   const int nbr = (int)hp.br_depth.size();
   P.T = cx, P.U = cu, P.nbranch = nbr;
   P.bdim = 0;
-  for (int b = 0; b < nbr; ++b) P.bdim += hp.br_depth[b] < NB;
+  for (int b = 0; b < nbr; ++b) P.bdim += hp.br_depth[b] < NBt;
   P.ncones = 1;
   for (int b = 0; b < nbr; ++b)
-    if (hp.br_depth[b] < NB) P.ncones += m;
+    if (hp.br_depth[b] < NBt) P.ncones += m;
   if (P.ncones > 32) return "too many cones (m^NB too large)";
 
   // ---- nodes ------------------------------------------------------------------------------
@@ -169,7 +179,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   std::vector<std::vector<int>> succ(T);
   for (int b = 0; b < nbr; ++b) {
     const int len = hp.br_len[b], ndx = hp.br_ndx[b], ndu = hp.br_ndu[b];
-    const bool leaf = hp.br_depth[b] == NB;
+    const bool leaf = hp.br_depth[b] == NBt;
     const int lvl0 = b == 0 ? 0 : 1 + (hp.br_depth[b] - 1) * N;
     for (int j = 0; j < len; ++j) {
       hp.x_u[ndx + j] = ndu + j;
@@ -248,7 +258,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   // ---- cones (buildIneqConstr :1940-1984): children of non-leaf branches, then the root ----
   int row = P.nlp, k = 0;
   for (int b = 0; b < nbr; ++b) {
-    if (hp.br_depth[b] >= NB) continue;
+    if (hp.br_depth[b] >= NBt) continue;
     for (int i = 0; i < m; ++i) {
       const int c = hp.br_child0[b] + i;
       hp.cone_b.push_back(b);
@@ -343,7 +353,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   const int nv = P.nv, neq = P.neq, nr = P.nrows, nc = P.ncones;
   L.uLin = take((size_t)(U + 1) * d);
   L.pprev = take((size_t)bd * m);
-  L.misc = take(8);
+  L.misc = take(8 + BMPC_MAX_N);
   L.xpred = take((size_t)T * n);
   L.upred = take((size_t)U * d);
   L.sol = take(nv);
@@ -353,8 +363,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.Ad = take((size_t)U * n * n);
   L.Bd = take((size_t)U * n * d);
   L.Cd = take((size_t)U * n);
-  L.dh = take((size_t)T * n);
-  L.h0 = take(T);
+  L.dh = take((size_t)T * P.Ncol * n);
+  L.h0 = take((size_t)T * P.Ncol);
   L.w = take(nbr);
   L.p = take((size_t)bd * m);
   L.boost = take(nc);
@@ -422,6 +432,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   } else {
     L.qo = L.qq = L.Pa = L.Ka = L.la = 0;
   }
+  L.xlin = robust ? take((size_t)T * n) : 0;
+  L.zrob = robust ? take((size_t)(T - 1) * P.Ncol * n) : 0;
   L.stride = o;
   return "";
 }

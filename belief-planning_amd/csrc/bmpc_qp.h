@@ -26,6 +26,15 @@ struct QpCtx {
 // u node whose input created x node k's state (the rate-cost predecessor of x_u[k]); -1 root
 BMPC_HD int qp_pred_u(CPlan& P, int u) { return P.t.x_srcu[P.t.u_x[u]]; }
 
+// coefficient j of inequality row c of state node k: Ncol collision rows (-dh) then the Fx rows
+template <int NX>
+BMPC_HD double qp_row(CPlan& P, const gdouble* dh, int k, int c, int j) {
+  return c < P.Ncol ? -dh[((size_t)k * P.Ncol + c) * NX + j] : P.desc.Fx[(c - P.Ncol) * NX + j];
+}
+// rows of state node k are live: every node with an input, and robustMPC's terminal node
+// (its Fx rows carry slacks, MPC_branch.py:1470-1472); BranchMPC's leaf terminals are empty
+BMPC_HD bool qp_rows_on(CPlan& P, int k) { return P.t.x_u[k] >= 0 || P.desc.controller == BMPC_CTRL_ROBUST; }
+
 // ---- cost, rhs (buildCost / buildIneqConstr / buildEqConstr of the current tree) ----------
 template <class X, class M>
 BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
@@ -51,8 +60,11 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
   gdouble* q = ws + L.qq;
   // BranchMPCProx: dQ = 3Q (:270); BranchMPC: dQ = 0.5Q, leaf's last node tracks xRef with Qf
   // and the leaf terminal node has no linear term (:1068-1099)
-  const bool prox = P.desc.controller == BMPC_CTRL_PROX;
-  const double dq = prox ? 3.0 : 0.5;
+  // robustMPC: unweighted Q (Qf on the terminal node) tracking xRef, no proximal term
+  // (buildCost :1540-1569)
+  const bool robust = P.desc.controller == BMPC_CTRL_ROBUST;
+  const bool prox = P.desc.controller == BMPC_CTRL_PROX || robust;
+  const double dq = robust ? 0.0 : P.desc.controller == BMPC_CTRL_PROX ? 3.0 : 0.5;
   // state nodes: Hx (doubled) and qx
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int b = t.x_branch[k];
@@ -72,7 +84,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
       }
       q[P.oX + k * NX + c] = v;
     }
-    for (int c = 0; c < Nc; ++c) q[P.oS + k * Nc + c] = term ? 0.0 : P.desc.Qslack[1] * wb;
+    for (int c = 0; c < Nc; ++c) q[P.oS + k * Nc + c] = qp_rows_on(P, k) ? P.desc.Qslack[1] * wb : 0.0;
   }
   // input nodes: diagonal blocks (doubled), rate couplings with the predecessor, qu
   const auto R = P.desc.R;
@@ -85,7 +97,12 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
     double D[NU][NU];
     for (int r = 0; r < NU; ++r)
       for (int c = 0; c < NU; ++c) D[r][c] = 0.0;
-    if ((leaf && j == len - 1) || !prox) {   // assigned w R (BranchMPC: every block, :1077-1090)
+    if (robust) {   // R + 2 dR, the last input R + dR (:1545-1549)
+      for (int r = 0; r < NU; ++r) {
+        for (int c = 0; c < NU; ++c) D[r][c] = R[r * NU + c];
+        D[r][r] += (u < P.U - 1 ? 2.0 : 1.0) * dR[r];
+      }
+    } else if ((leaf && j == len - 1) || !prox) {   // assigned w R (BranchMPC: every block, :1077-1090)
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) D[r][c] = wb * R[r * NU + c];
     } else {
@@ -95,7 +112,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
         if (j >= 1 || b != 0) D[r][r] += wb * dR[r];
       }
     }
-    if (u == 0 && prox)   // Hu[0:d,0:d] += dR (row broadcast), upper triangle read by OSQP
+    if (u == 0 && prox && !robust)   // Hu[0:d,0:d] += dR (row broadcast), upper triangle read by OSQP
       for (int r = 0; r < NU; ++r)
         for (int c = 0; c < NU; ++c) D[r][c] += dR[r > c ? r : c];
     gdouble* Hu = ws + L.hu + u * NU * NU;
@@ -109,13 +126,14 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
     double od = 0.0;
     if (u == 0)
       for (int r = 0; r < NU; ++r) od += ws[L.misc + MISC_OLDU + r] * dR[r];
-    for (int c = 0; c < NU; ++c) q[P.oU + u * NU + c] = u == 0 ? -2.0 * od : 0.0;
+    for (int c = 0; c < NU; ++c)   // robustMPC: -2 OldInput diag(dR), a vector (:1559)
+      q[P.oU + u * NU + c] = u != 0 ? 0.0 : robust ? -2.0 * ws[L.misc + MISC_OLDU + c] * dR[c] : -2.0 * od;
   }
   // rhs of the inequalities: [h0 | bx] per non-terminal node, bu per input, 0 for -S
   const gdouble* h0 = ws + L.h0;
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
     const int k = it / Nc, c = it % Nc;
-    hv[P.rFx + it] = t.x_u[k] < 0 ? 0.0 : (c == 0 ? h0[k] : P.desc.bx[c - 1]);
+    hv[P.rFx + it] = !qp_rows_on(P, k) ? 0.0 : c < P.Ncol ? h0[k * P.Ncol + c] : P.desc.bx[c - P.Ncol];
     hv[P.rPos + it] = 0.0;
   }
   for (int it = ex.lane; it < P.U * P.nFu; it += ex.nlanes) hv[P.rFu + it] = P.desc.bu[it % P.nFu];
@@ -123,7 +141,9 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
   const gdouble* Cd = ws + L.Cd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const int su = t.x_srcu[k];
-    for (int r = 0; r < NX; ++r) bv[k * NX + r] = su >= 0 ? Cd[su * NX + r] : xbar[r];
+    // x_0 = x: robustMPC linearises about the shifted prediction, so x is kept apart
+    const gdouble* x0 = robust ? ws + L.misc + MISC_X0 : xbar;
+    for (int r = 0; r < NX; ++r) bv[k * NX + r] = su >= 0 ? Cd[su * NX + r] : x0[r];
   }
   ex.sync();
 }
@@ -185,8 +205,8 @@ BMPC_FN void qp_apply_G(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     double v = -zv[P.oS + it];
-    if (t.x_u[k] >= 0)
-      for (int j = 0; j < NX; ++j) v += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * zv[P.oX + k * NX + j];
+    if (qp_rows_on(P, k))
+      for (int j = 0; j < NX; ++j) v += qp_row<NX>(P, dh, k, c, j) * zv[P.oX + k * NX + j];
     return v;
   }, [&](int it, double v) { out[P.rFx + it] = v; });
   lane_batch(ex, 0, P.U * P.nFu, [&](int it) {
@@ -214,8 +234,8 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble*
     const bool term = t.x_u[k] < 0;
     for (int c = 0; c < Nc; ++c) {
       const double rv = r[P.rFx + k * Nc + c];
-      if (!term)
-        for (int j = 0; j < NX; ++j) ax[j] += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * rv;
+      if (qp_rows_on(P, k))
+        for (int j = 0; j < NX; ++j) ax[j] += qp_row<NX>(P, dh, k, c, j) * rv;
       out[P.oS + k * Nc + c] = -rv - r[P.rPos + k * Nc + c];
     }
     for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = ax[j];
@@ -322,12 +342,12 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
         // reduced x Hessian: Hx + sum_c omega_c f_c f_c'
         double Hx[NX][NX];
         mat_load(Hx, ws + L.hx + k * NX * NX);
-        if (!term)
+        if (qp_rows_on(P, k))
           for (int c = 0; c < Nc; ++c) {
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double om = df - df * df / sd;
             double f[NX];
-            for (int j = 0; j < NX; ++j) f[j] = c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j];
+            for (int j = 0; j < NX; ++j) f[j] = qp_row<NX>(P, dh, k, c, j);
             for (int i = 0; i < NX; ++i)
               for (int j = 0; j < NX; ++j) Hx[i][j] += om * f[i] * f[j];
           }
@@ -455,11 +475,11 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
         const bool term = t.x_u[k] < 0;
         double qx[NX];
         for (int j = 0; j < NX; ++j) qx[j] = -r[P.oX + k * NX + j];
-        if (!term)
+        if (qp_rows_on(P, k))
           for (int c = 0; c < Nc; ++c) {   // slack elimination
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double a = df * r[P.oS + k * Nc + c] / sd;
-            for (int j = 0; j < NX; ++j) qx[j] -= (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * a;
+            for (int j = 0; j < NX; ++j) qx[j] -= qp_row<NX>(P, dh, k, c, j) * a;
           }
         double lt[NS];
         if (term) {
@@ -542,8 +562,8 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
         for (int c = 0; c < Nc; ++c) {   // slack recovery
           const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
           double fx = 0.0;
-          if (!term)
-            for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * s[j];
+          if (qp_rows_on(P, k))
+            for (int j = 0; j < NX; ++j) fx += qp_row<NX>(P, dh, k, c, j) * s[j];
           out[P.oS + k * Nc + c] = (r[P.oS + k * Nc + c] + df * fx) / sd;
         }
         if (term) break;
@@ -764,7 +784,19 @@ BMPC_HD IpmResult solve_ego_qp(const X& ex, const Plan& P, const Layout& L, EgoV
   QpCtx C{(CPlan*)&P, (CLayout*)&L, ws};
   qp_build<X, M>(ex, C, ws + L.hvec, ws + L.bvec);
   IpmResult r = qp_ipm<X, NX, NU>(ex, C);
-  if (r.exit_flag == 1) {
+  if (P.desc.controller == BMPC_CTRL_ROBUST) {
+    // unpackSolution takes the solution whatever the status (:1459-1465); the next solve
+    // linearises about the prediction shifted by one step (:1429-1431)
+    const gdouble* sol = ws + L.sol;
+    for (int i = ex.lane; i < P.U * NU; i += ex.nlanes) {
+      ws[L.upred + i] = sol[P.oU + i];
+      ws[L.uLin + i] = sol[P.oU + (i / NU + 1 < P.U ? i + NU : i)];
+    }
+    for (int i = ex.lane; i < P.T * NX; i += ex.nlanes) {
+      ws[L.xpred + i] = sol[P.oX + i];
+      ws[L.xlin + i] = sol[P.oX + (i / NX + 1 < P.T ? i + NX : i)];
+    }
+  } else if (r.exit_flag == 1) {
     const gdouble* sol = ws + L.sol;
     for (int i = ex.lane; i < P.U * NU; i += ex.nlanes) {
       const double v = sol[P.oU + i];

@@ -57,7 +57,7 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
 template <class X, class M>
 BMPC_HD IpmResult solve_ego(const X& ex, const Plan& P, const Layout& L, EgoView E,
                             const double* x, const double* z, const double* xref) {
-  tree_update<X, M>(ex, P, L, E, x, z, xref);
+  tree_step<X, M>(ex, P, L, E, x, z, xref);
   if (P.desc.controller != BMPC_CTRL_CVAR) return solve_ego_qp<X, M>(ex, P, L, E);
   return solve_ego_ipm<X, M>(ex, P, L, E);
 }

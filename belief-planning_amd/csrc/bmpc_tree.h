@@ -153,4 +153,90 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
   ex.sync();
 }
 
+// robustMPC (MPC_branch.py:1275-1443): the chain's linearisation trajectory -- the carried
+// shifted prediction, or on the first solve the rollout of u = 0 from x (get_xLin :1326) --
+// its dynamics (computeLTVdynamics :1438), the obstacle predictions of every time slot
+// (inittree/updatetree :1336-1383: slot 0 the measured z, slot (D-1)N+i+1 the m^D
+// predictions of depth D in BFS order) and one collision row per prediction
+// (buildIneqConstr :1474-1483).  Rows past a slot's prediction count are padding: dh = 0 and
+// h0 = 1, inactive at the optimum (their slack is 0, the row slack 1).
+template <class X, class M>
+BMPC_HD void tree_update_robust(const X& ex, const Plan& P, const Layout& L, EgoView E,
+                                const double* x, const double* z, const double* xref) {
+  constexpr int NX = M::NX, NU = M::NU;
+  const int N = P.N, m = P.m, T = P.T, U = P.U, Ncol = P.Ncol;
+  double* ws = E.ws;
+  double* xbar = ws + L.xbar;
+  double* ubar = ws + L.ubar;
+  double* zr = ws + L.zrob;
+  const bool init = ws[L.misc + MISC_INIT] != 0.0;
+  const double dt = P.desc.dt;
+  const double* mc = P.desc.mc;
+  for (int i = ex.lane; i < NX; i += ex.nlanes) {
+    ws[L.misc + MISC_X0 + i] = x[i];
+    ws[L.xref + i] = xref[i];
+    zr[i] = z[i];
+  }
+  if (ex.lane == 0) ws[L.w] = 1.0;
+  if (init) {
+    for (int i = ex.lane; i < T * NX; i += ex.nlanes) xbar[i] = ws[L.xlin + i];
+    for (int i = ex.lane; i < U * NU; i += ex.nlanes) ubar[i] = ws[L.uLin + i];
+  } else {
+    for (int i = ex.lane; i < U * NU; i += ex.nlanes) ubar[i] = 0.0;
+    if (ex.lane == 0) {
+      double xc[NX], u0[NU];
+      for (int k = 0; k < NU; ++k) u0[k] = 0.0;
+      for (int k = 0; k < NX; ++k) xc[k] = xbar[k] = x[k];
+      for (int i = 1; i < T; ++i) {
+        step<M>(dt, xc, u0, xbar + i * NX);
+        for (int k = 0; k < NX; ++k) xc[k] = xbar[i * NX + k];
+      }
+    }
+  }
+  ex.sync();
+  for (int u = ex.lane; u < U; u += ex.nlanes) {
+    double xp[NX];
+    linearize<M>(dt, xbar + u * NX, ubar + u * NU, ws + L.Ad + u * NX * NX, ws + L.Bd + u * NX * NU,
+                 ws + L.Cd + u * NX, xp);
+  }
+  // obstacle predictions, depth by depth: prediction j of depth D continues prediction j/m of
+  // depth D-1 (its slot (D-1)N) under policy j%m
+  int nd = 1;
+  for (int D = 1; D <= P.zNB; ++D) {
+    nd *= m;
+    const int s0 = (D - 1) * N;
+    for (int j = ex.lane; j < nd; j += ex.nlanes)
+      rollout<M>(dt, N, E.pol[j % m], zr + ((size_t)s0 * Ncol + j / m) * NX, zr + ((size_t)(s0 + 1) * Ncol + j) * NX,
+                 Ncol * NX);
+    ex.sync();
+  }
+  double* dh = ws + L.dh;
+  double* h0 = ws + L.h0;
+  for (int it = ex.lane; it < T * Ncol; it += ex.nlanes) {
+    const int k = it / Ncol, j = it % Ncol;
+    int cnt = 0;
+    if (k == 0) {
+      cnt = 1;
+    } else if (k < T - 1) {
+      cnt = 1;
+      for (int D = (k - 1) / N + 1; D > 0; --D) cnt *= m;
+    }
+    if (j < cnt) {
+      col_eval<M>(mc, xbar + k * NX, zr + (size_t)it * NX, h0 + it, dh + (size_t)it * NX);
+    } else {
+      h0[it] = 1.0;
+      for (int c = 0; c < NX; ++c) dh[(size_t)it * NX + c] = 0.0;
+    }
+  }
+  ex.sync();
+}
+
+// the tree step of the plan's controller
+template <class X, class M>
+BMPC_HD void tree_step(const X& ex, const Plan& P, const Layout& L, EgoView E, const double* x, const double* z,
+                       const double* xref) {
+  if (P.desc.controller == BMPC_CTRL_ROBUST) tree_update_robust<X, M>(ex, P, L, E, x, z, xref);
+  else tree_update<X, M>(ex, P, L, E, x, z, xref);
+}
+
 }  // namespace bmpc

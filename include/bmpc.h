@@ -53,7 +53,11 @@ extern "C" {
 enum {
   BMPC_CTRL_CVAR = 0, /* BranchMPC_CVaR  (ECOS SOCP)   MPC_branch.py:1598 */
   BMPC_CTRL_PROX = 1, /* BranchMPCProx   (OSQP QP)     MPC_branch.py:82   */
-  BMPC_CTRL_QP = 2    /* BranchMPC, active definition (OSQP QP) MPC_branch.py:881 */
+  BMPC_CTRL_QP = 2,   /* BranchMPC, active definition (OSQP QP) MPC_branch.py:881 */
+  BMPC_CTRL_ROBUST = 3 /* robustMPC: one input sequence against every obstacle prediction
+                          of the tree (OSQP QP) MPC_branch.py:1275.  T = N*NB+2 states,
+                          U = N*NB+1 inputs, no branch weights; status 1 = solved, the
+                          solution is taken whatever the status (:1459) */
 };
 
 /* predictive models */
@@ -167,6 +171,12 @@ int bmpc_solve_device(bmpc_plan* plan, const double* d_x, const double* d_z,
  * updatetree, not inittree); NULL p / jcons / old_input keep the current values; mask NULL
  * = all egos. */
 int bmpc_get_warm_start(bmpc_plan* plan, double* uLin, double* p, double* jcons, double* old_input);
+/* robustMPC's warm start: the linearisation trajectory xLin [batch][T][n] and uLin
+ * [batch][U][d] (the previous prediction shifted by one step, MPC_branch.py:1429-1431) and
+ * OldInput [batch][d]; set marks the egos initialised; get/set NULL pointers skip. */
+int bmpc_get_robust_warm_start(bmpc_plan* plan, double* xLin, double* uLin, double* old_input);
+int bmpc_set_robust_warm_start(bmpc_plan* plan, const double* xLin, const double* uLin,
+                               const double* old_input, const uint8_t* mask);
 int bmpc_set_warm_start(bmpc_plan* plan, const double* uLin, const double* p,
                         const double* jcons, const double* old_input, const uint8_t* mask);
 

@@ -137,6 +137,20 @@ int hs_set_warm_start(void* p, const double* uLin, const double* pprev, const do
   return 0;
 }
 
+int hs_set_robust_warm_start(void* p, const double* xlin, const double* ulin, const double* oldu) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  for (int e = 0; e < h->batch; ++e) {
+    double* ws = h->ws.data() + L.stride * e;
+    memcpy(ws + L.xlin, xlin + (size_t)e * P.T * P.n, sizeof(double) * P.T * P.n);
+    memcpy(ws + L.uLin, ulin + (size_t)e * P.U * P.d, sizeof(double) * P.U * P.d);
+    memcpy(ws + L.misc + MISC_OLDU, oldu + (size_t)e * P.d, sizeof(double) * P.d);
+    ws[L.misc + MISC_INIT] = 1.0;
+  }
+  return 0;
+}
+
 // debugging aids: raw workspace of ego e and the Layout offsets (sizeof(Layout)/8 size_t)
 double* hs_ws_ptr(void* p, int e) {
   HS* h = (HS*)p;

@@ -110,6 +110,10 @@ class HostSim:
         oldu = None if oldu is None else np.ascontiguousarray(np.asarray(oldu, float).reshape(B, self.desc.d))
         lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons), _p(oldu))
 
+    def set_robust_warm_start(self, xlin, ulin, oldu):
+        xlin, ulin, oldu = (np.ascontiguousarray(a, dtype=np.float64) for a in (xlin, ulin, oldu))
+        lib().hs_set_robust_warm_start(self.h, _p(xlin), _p(ulin), _p(oldu))
+
     def reset_mask(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         lib().hs_reset(self.h, _p(m))

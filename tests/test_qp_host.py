@@ -8,6 +8,7 @@ OSQP itself is absent and unpinned; the oracle returns the exact QP 
 must be 1 on every step; uPred[0] to 1e-6 absolute (|u| <= 0.5); the full primal vector of
 the kept steps to 1e-6 relative to max(1, |z|)."""
 import numpy as np
+import pytest
 
 import hostsim_lib as H
 from common import golden, quad_replay_batch, quadruped_desc_from_golden, quadruped_policy_rows
@@ -51,3 +52,33 @@ def test_branch_mpc_qp_replay():
     for t in (int(k) for k in g["keep"]):
         ref = g[f"s{t}_sol"]
         np.testing.assert_allclose(sol[t], ref, atol=1e-6 * max(1.0, np.abs(ref).max()), err_msg=f"step {t}")
+
+
+def _robust_desc(g):
+    from common import highway_desc_from_golden
+    from bmpc import abi
+    desc = highway_desc_from_golden(g)
+    desc.controller = abi.CTRL_ROBUST
+    return desc
+
+
+@pytest.mark.parametrize("name", ["highway_robust_n20_nb1", "highway_robust_n8_nb2"])
+def test_robust_mpc_replay(name):
+    """robustMPC (MPC_branch.py:1275): every recorded step replayed as one ego carrying the
+    reference's warm start (shifted prediction, OldInput); uPred/xPred of every step to 1e-6
+    (the oracle QP optimum stands in for OSQP + polish), the kept steps' full primal
+    vector against the reference's OSQP problem solution on its x/u part."""
+    from common import highway_policy_rows
+    g = golden(name)
+    T = len(g["traj_x"])
+    hs = H.HostSim(_robust_desc(g), T)
+    assert (hs.T, hs.U) == (g["traj_xPred"].shape[1], g["traj_uPred"].shape[1])
+    hs.set_policies(highway_policy_rows(g["traj_lc_target"], float(g["Kpsi"])))
+    xl = np.asarray(g["traj_ws_xLin"], float)
+    warm = ~np.isnan(xl).any(axis=(1, 2))
+    hs.set_robust_warm_start(np.nan_to_num(xl), np.nan_to_num(g["traj_ws_uLin"]), g["traj_ws_old"])
+    hs.reset_mask(~warm)
+    r = hs.solve(g["traj_x"], g["traj_z"], g["traj_xRef"])
+    np.testing.assert_array_equal(r["status"], g["traj_status"])
+    np.testing.assert_allclose(r["upred"], g["traj_uPred"], atol=1e-6)
+    np.testing.assert_allclose(r["xpred"], g["traj_xPred"], atol=1e-6)
