@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("highway", "quadruped"), default="highway",
+    ap.add_argument("--workload", choices=("highway", "quadruped", "robust"), default="highway",
                     help="highway = BASELINE metric config; quadruped = BASELINE config 4 (BranchMPCProx)")
     ap.add_argument("--batch", type=int, default=None, help="egos per GPU (highway 4096, quadruped 1024)")
     ap.add_argument("--N", type=int, default=None)
@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
     a = ap.parse_args()
     quad = a.workload == "quadruped"
+    robust = a.workload == "robust"     # robustMPC (MPC_branch.py:1275) in the same scene
     a.batch = a.batch or (1024 if quad else 4096)
     a.N = a.N or (25 if quad else 20)
     a.NB = a.NB or (2 if quad else 1)
@@ -154,6 +155,8 @@ def main():
     else:
         x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(B * world, seed=0))
         desc = highway_desc(N=a.N, NB=a.NB)
+        if robust:
+            desc.controller = abi.CTRL_ROBUST
         pl = plan.BatchPlan(desc, B, device=local)
         pl.set_policies(highway_policy_rows(tgt))
     tx = torch.tensor(x, device=dev, dtype=torch.float64)
@@ -250,27 +253,35 @@ def main():
         if quad:   # same per-node formula, n = d = 3, Nc = 1, nFu = 6, no cones, m = 2
             F_it = flops_per_iter(T, 3, 3, 1, 6, [])
             F_mod = flops_model(U, nbr - 1, bdim, 2, a.N, 3)
+        elif robust:   # chain of T nodes, Nc = 4 Fx rows + 3^NB collision rows, no cones
+            F_it = flops_per_iter(T, 4, 2, 4 + 3 ** a.NB, 4, [])
+            F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
         else:
             cone_dims = [2 + a.N * 6] * (bdim * 3) + [4]
             F_it = flops_per_iter(T, 4, 2, 5, 4, cone_dims)
             F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
         achieved = B * iters_mean * F_it / (tm["ipm_ms"] * 1e-3) / 1e12 if tm["ipm_ms"] > 0 else 0.0
-        traffic = None if quad else load_traffic(a.traffic)
+        traffic = None if (quad or robust) else load_traffic(a.traffic)
         out = {
-            "metric": METRIC if not quad else "branch-MPC solves/sec (whole node), quadruped BranchMPCProx "
-                                              "N=25 NB=2 m=2 (4 leaves), batch 1024 egos",
+            "metric": (METRIC if not (quad or robust) else
+                       "branch-MPC solves/sec (whole node), quadruped BranchMPCProx N=25 NB=2 m=2 (4 leaves), "
+                       "batch 1024 egos" if quad else
+                       f"robustMPC solves/sec (whole node), highway N={a.N} NB={a.NB}, {3 ** a.NB} obstacle "
+                       f"predictions per slot, batch {B} egos"),
             "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)",
             "config": {"workload": (f"quadruped BranchMPCProx closed loop, N={a.N}, NB={a.NB}, m=2 " if quad else
+                                    f"highway robustMPC closed loop, N={a.N}, NB={a.NB}, m=3 " if robust else
                                     f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
                                    + f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"ego-sharded dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
                          "traffic": traffic,
-                         "kernel": "k_qp (structured Mehrotra QP IPM)" if quad else "k_ipm (structured HSDE IPM)",
+                         "kernel": "k_qp (structured Mehrotra QP IPM)" if (quad or robust) else
+                                   "k_ipm (structured HSDE IPM)",
                          "kernel_ms": round(tm["ipm_ms"], 4),
                          "tree_kernel_ms": round(tm["tree_ms"], 4),
                          "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
@@ -282,7 +293,7 @@ def main():
                             "collision_steps": int(st_h[abi.ENVS_COLL_STEPS]),
                             "env": "device k_env (sim_overtake scene)" if not quad else "torch ops"},
         }
-        if not a.no_cpu_baseline and world == 1 and not quad:
+        if not a.no_cpu_baseline and world == 1 and not (quad or robust):
             procs = max(1, min(8, len(os.sched_getaffinity(0))))
             cb = cpu_baseline(a.N, a.NB, a.cpu_sample, procs)
             out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
