@@ -1854,10 +1854,12 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       // combined: ds_comb = -lam o lam - dsW_a o Wdz_a + sigma mu e
       jprod(ex, C, lam, lam, ra);
       jprod(ex, C, ds, rb, rc);
-      lane_batch<8>(ex, 0, nr, [&](int i) { return -ra[i] - rc[i]; }, [&](int i, double v) { ra[i] = v; });
+      lane_batch<8>(ex, 0, nr, [&](int i) {
+        const double v = -ra[i] - rc[i];
+        return i < P.nlp ? v + (sigma * mu) : v;   // + sigma mu e on the LP rows
+      }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
-      lane_batch(ex, 0, P.nlp, [&](int i) { return ra[i] + (sigma * mu); }, [&](int i, double v) { ra[i] = v; });
-      for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;
+      for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;   // ... and cone heads
       ex.sync();
       jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
       apply_W(ex, C, 0, ds, rb, -1.0, rz, eta1);               // eta1 rz - W xi
@@ -1867,7 +1869,11 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       kkt_solve<X, NX, NU>(ex, C, tA, ya, rb, x2, y2, z2, nref);
       const double dk_c = -kap * tau - dtau_a * dkap_a + sigma * mu;
       dtau = (eta1 * rt + dk_c / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
-      lane_batch<8>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) { x2[i] = v; });
+      double nonfinite = 0.0;   // the step's finiteness check, taken in the pass that forms dx
+      lane_batch<8>(ex, 0, nv, [&](int i) { return x2[i] + (dtau * x1[i]); }, [&](int i, double v) {
+        x2[i] = v;
+        if (!isfinite(v)) nonfinite = 1.0;
+      });
       lane_batch(ex, 0, neq, [&](int i) { return y2[i] + (dtau * y1[i]); }, [&](int i, double v) { y2[i] = v; });
       lane_batch<8>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
       ex.sync();
@@ -1881,9 +1887,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       a = fmin(a, 0.999);
       alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
       apply_W(ex, C, 0, ds, rb);                               // ds = W dsW
-      double fin = 0.0;
-      fin = strided_partial<8, 1>(ex.lane, ex.nlanes, nv, [&](int i) { return isfinite(x2[i]) ? 0.0 : 1.0; });
-      fin = ex.max(fin);
+      const double fin = ex.max(nonfinite);
       ok = fin == 0.0 && isfinite(dtau) && alpha > 1e-10;
       if (ok) {
         lane_batch<8>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
