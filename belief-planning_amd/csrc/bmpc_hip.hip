@@ -251,7 +251,11 @@ struct bmpc_plan {
   hipStream_t stream = nullptr;
   hipStream_t user_stream = nullptr;
   bool timing = false;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // timing ring: three events per instrumented solve, read back only when the ring is full
+  // or bmpc_timing is called, so timed solves run without a host synchronisation
+  static constexpr int kTimeSlots = 32;
+  hipEvent_t ev[3 * kTimeSlots] = {};
+  int t_pending = 0;
   double t_acc[2] = {0, 0};
   int t_cnt = 0;
   bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
@@ -398,6 +402,23 @@ int bmpc_reset(bmpc_plan* pl, const uint8_t* mask) {
   return 0;
 }
 
+
+// Reads back the pending timing events (waits for the last instrumented solve).
+static int fold_timing(bmpc_plan* pl) {
+  for (int k = 0; k < pl->t_pending; ++k) {
+    hipEvent_t* ev = pl->ev + 3 * k;
+    HIPCHECK(hipEventSynchronize(ev[2]));
+    float a = 0, b = 0;
+    HIPCHECK(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIPCHECK(hipEventElapsedTime(&b, ev[1], ev[2]));
+    pl->t_acc[0] += a;
+    pl->t_acc[1] += b;
+    pl->t_cnt += 1;
+  }
+  pl->t_pending = 0;
+  return 0;
+}
+
 static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
                         double* d_upred, double* d_xpred, double* d_bw, double* d_J,
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
@@ -410,7 +431,8 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     const size_t want = (size_t)atol(e);
     if (want > lds_bytes && want <= 160 * 1024) lds_bytes = want;
   }
-  if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[0], s));
+  hipEvent_t* ev = pl->ev + 3 * pl->t_pending;
+  if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_x, d_z, d_xref, B);
@@ -418,7 +440,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     hipLaunchKernelGGL(k_tree<Quadruped>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_x, d_z, d_xref, B);
   HIPCHECK(hipGetLastError());
-  if (pl->timing) HIPCHECK(hipEventRecord(pl->ev[1], s));
+  if (pl->timing) HIPCHECK(hipEventRecord(ev[1], s));
   const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(qp ? k_qp<Highway> : k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
@@ -428,14 +450,8 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                        pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   HIPCHECK(hipGetLastError());
   if (pl->timing) {
-    HIPCHECK(hipEventRecord(pl->ev[2], s));
-    HIPCHECK(hipEventSynchronize(pl->ev[2]));
-    float a = 0, b = 0;
-    HIPCHECK(hipEventElapsedTime(&a, pl->ev[0], pl->ev[1]));
-    HIPCHECK(hipEventElapsedTime(&b, pl->ev[1], pl->ev[2]));
-    pl->t_acc[0] += a;
-    pl->t_acc[1] += b;
-    pl->t_cnt += 1;
+    HIPCHECK(hipEventRecord(ev[2], s));
+    if (++pl->t_pending == bmpc_plan::kTimeSlots) return fold_timing(pl);
   }
   return 0;
 }
@@ -636,6 +652,7 @@ int bmpc_get_tree(bmpc_plan* pl, double* xbar, double* ubar, double* zbar, doubl
 int bmpc_enable_timing(bmpc_plan* pl, int on) {
   if (!pl) return fail(-22, "null argument");
   pl->timing = on != 0;
+  pl->t_pending = 0;
   pl->t_acc[0] = pl->t_acc[1] = 0;
   pl->t_cnt = 0;
   return 0;
@@ -643,6 +660,7 @@ int bmpc_enable_timing(bmpc_plan* pl, int on) {
 
 int bmpc_timing(bmpc_plan* pl, double* ms, int32_t* count) {
   if (!pl) return fail(-22, "null argument");
+  if (int rc = fold_timing(pl)) return rc;
   const int c = pl->t_cnt;
   if (ms) {
     ms[0] = c ? pl->t_acc[0] / c : 0.0;

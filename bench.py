@@ -224,14 +224,11 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    # per-kernel device timing over separate instrumented steps (HIP events on the launch
-    # stream); the timed region below runs without event synchronisation
+    # per-kernel device timing over the timed steps themselves: HIP events recorded on the
+    # launch stream around each kernel, read back after the region (no host synchronisation
+    # inside it); the IPM iteration mean comes from the same launches
+    it_sum = torch.zeros(B, dtype=torch.float64, device=dev)
     pl.enable_timing(True)
-    for _ in range(3):
-        step()
-    tm = pl.timing()
-    pl.enable_timing(False)
-    iters_mean = float(it.double().mean().item())
     estats.zero_()
     if world > 1:
         dist.barrier()
@@ -239,12 +236,16 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+        it_sum.add_(it)
     stats = estats.sum(0)
     D.reduce_stats(stats)        # the only collective
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+    tm = pl.timing()
+    pl.enable_timing(False)
+    iters_mean = float(it_sum.sum().item()) / (B * max(a.steps, 1))
     total = B * world * a.steps
     value = total / elapsed
     if rank == 0:

@@ -188,7 +188,8 @@ int bmpc_get_tree(bmpc_plan* plan, double* xbar, double* ubar, double* zbar, dou
 
 /* Average device time per call of each kernel over the solves since the last call
  * (HIP events on the launch stream); ms[0] = tree/linearisation kernel, ms[1] = IPM
- * kernel, count = number of solves timed.  Timing must be enabled first. */
+ * kernel, count = number of solves timed.  Timing must be enabled first.  Timed solves do
+ * not synchronise the host: events are read back every 32 solves and by bmpc_timing. */
 int bmpc_enable_timing(bmpc_plan* plan, int on);
 int bmpc_timing(bmpc_plan* plan, double* ms /* [2] */, int32_t* count);
 
