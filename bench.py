@@ -272,7 +272,8 @@ def main():
             "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)",
+            "data": ("synthetic (seeded quadruped egos, seed 1; obstacle on the forward policy)" if quad
+                     else "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)"),
             "config": {"workload": (f"quadruped BranchMPCProx closed loop, N={a.N}, NB={a.NB}, m=2 " if quad else
                                     f"highway robustMPC closed loop, N={a.N}, NB={a.NB}, m=3 " if robust else
                                     f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
