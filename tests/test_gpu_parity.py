@@ -188,3 +188,26 @@ def test_hmm_eval_matches_oracle(gpu):
     for M, m in ((1, 3), (2, 3), (4, 4)):
         xb, u, xbk = _hmm_case(M * 10 + m, M, m, 64)
         check_hmm_against_oracle(gpu.hmm_eval(M, m, HC, xb, u, xbk), M, m, xb, u, xbk)
+
+
+def test_kernel_timing_ring(gpu):
+    """bmpc_enable_timing / bmpc_timing: 40 timed solves (more than the 32-slot event ring, so the
+    ring is read back once inside a solve and once by bmpc_timing) are all counted, with positive
+    per-kernel averages; the timed solves' results equal untimed ones."""
+    B = 8
+    x, z, xref, tgt = seeded_batch(B, seed=2)
+    desc = highway_desc(N=10, NB=1)
+    ref = gpu.BatchPlan(desc, B)
+    ref.set_policies(highway_policy_rows(tgt))
+    pl = gpu.BatchPlan(desc, B)
+    pl.set_policies(highway_policy_rows(tgt))
+    pl.enable_timing(True)
+    for _ in range(40):
+        r = pl.solve(x, z, xref)
+        q = ref.solve(x, z, xref)
+        np.testing.assert_array_equal(r["upred"], q["upred"])
+    tm = pl.timing()
+    assert tm["count"] == 40
+    assert tm["tree_ms"] > 0 and tm["ipm_ms"] > 0
+    assert pl.timing()["count"] == 0      # reading resets the accumulators
+    pl.enable_timing(False)
