@@ -116,7 +116,7 @@ class BranchMPC_CVaR:
         self.tree_index = TreeIndex(self.N, self.NB, self.m)
         self.totalx, self.totalu = self.tree_index.T, self.tree_index.U
         self.branchdim = self.tree_index.bdim
-        self.BT = None
+        self._bt = None
         self.xPred = self.uPred = self.xLin = self.uLin = None
         self.OldInput = np.zeros(self.d)
         self.feasible = 0
@@ -178,7 +178,7 @@ class BranchMPC_CVaR:
         self.xLin = self.xPred
         self.uLin = np.vstack((self.uPred, self.uPred[-1]))
         self.OldInput = self.uPred[0, :]
-        self.BT = None
+        self._bt = None            # rebuilt from the device tree on first access of .BT
         self._tree = None
 
     def solve_batch(self, X, Z, XREF):
@@ -214,6 +214,21 @@ class BranchMPC_CVaR:
                 us.append(np.vstack((a["ubar"][lu], a["ubar"][su])))
         return xs, zs, us, ws
 
+    @property
+    def BT(self):
+        """The live scenario tree of the last solve (``MPC_branch.py:65-78,2062-2064``):
+        built from the device tree on first access after a solve (``None`` before any)."""
+        if self._bt is None and self._last is not None and self._plan is not None:
+            try:
+                self.build_tree()
+            except NotImplementedError:
+                return None
+        return self._bt
+
+    @BT.setter
+    def BT(self, tree):
+        self._bt = tree
+
     def build_tree(self, e=0):
         """BranchTree objects of the last solve (the reference's ``self.BT``)."""
         t = self.tree_index
@@ -230,8 +245,8 @@ class BranchMPC_CVaR:
         for b in range(t.nbranch):
             for c in t.children[b]:
                 nodes[b].addchild(nodes[c])
-        self.BT = nodes[0]
-        return self.BT
+        self._bt = nodes[0]
+        return self._bt
 
     @property
     def Solution(self):

@@ -403,9 +403,13 @@ int bmpc_reset(bmpc_plan* pl, const uint8_t* mask) {
 }
 
 
-// Reads back the pending timing events (waits for the last instrumented solve).
+// Reads back the pending timing events (waits for the last instrumented solve).  The ring is
+// emptied on every exit path: a failed read-back drops the pending samples rather than leaving
+// t_pending at kTimeSlots (the next launch would index past ev[]).
 static int fold_timing(bmpc_plan* pl) {
-  for (int k = 0; k < pl->t_pending; ++k) {
+  const int pending = pl->t_pending;
+  pl->t_pending = 0;
+  for (int k = 0; k < pending && k < bmpc_plan::kTimeSlots; ++k) {
     hipEvent_t* ev = pl->ev + 3 * k;
     HIPCHECK(hipEventSynchronize(ev[2]));
     float a = 0, b = 0;
@@ -415,7 +419,6 @@ static int fold_timing(bmpc_plan* pl) {
     pl->t_acc[1] += b;
     pl->t_cnt += 1;
   }
-  pl->t_pending = 0;
   return 0;
 }
 
@@ -431,7 +434,9 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     const size_t want = (size_t)atol(e);
     if (want > lds_bytes && want <= 160 * 1024) lds_bytes = want;
   }
-  hipEvent_t* ev = pl->ev + 3 * pl->t_pending;
+  if (pl->timing && (pl->t_pending < 0 || pl->t_pending >= bmpc_plan::kTimeSlots))
+    return fail(-5, "timing ring out of range (t_pending = " + std::to_string(pl->t_pending) + ")");
+  hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,

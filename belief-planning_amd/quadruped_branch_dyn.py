@@ -14,8 +14,9 @@ from bmpc import abi
 from bmpc.tracing import PolicySpec, Tracer
 from highway_branch_dyn import PredictiveModel as _HighwayModel
 from highway_branch_dyn import propagate_backup, softmax, softmin, softsat  # noqa: F401
+from utils import Quad_constants  # noqa: F401  (re-exported: the reference star-imports it, :7)
 
-__all__ = ["np", "quad_kinetics", "softsat", "backup_forward", "backup_stop", "softmin", "softmax",
+__all__ = ["np", "Quad_constants", "quad_kinetics", "softsat", "backup_forward", "backup_stop", "softmin", "softmax",
            "propagate_backup", "robot_col", "PredictiveModel"]
 
 

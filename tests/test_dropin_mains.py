@@ -1,0 +1,109 @@
+"""The reference's own entry scripts run unchanged against the drop-in modules.
+
+``main_quadruped.py`` and ``main_branch.py`` are executed from ``/root/reference`` (this
+container only; skipped where the reference is absent, e.g. on the GPU box) with
+``belief-planning_amd`` first on ``sys.path``, so every ``import`` in them resolves to the
+build's modules.  Only the device calls are replaced: ``bmpc.plan.BatchPlan`` and
+``bmpc.plan.model_eval`` are swapped for the test-only host build of the same kernels
+(tests/hostsim), so the scripts run their full controller path on CPU.
+"""
+import os
+import runpy
+
+import numpy as np
+import pytest
+
+REF = "/root/reference"
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+
+
+class _HostPlan:
+    """BatchPlan stand-in over the host build (same methods the compat classes call)."""
+
+    solves = 0
+
+    def __init__(self, desc, batch, device=0):
+        import hostsim_lib
+        self.desc, self.batch = desc, batch
+        self._hs = hostsim_lib.HostSim(desc, batch)
+        self.T, self.U, self.bdim, self.nbranch = self._hs.T, self._hs.U, self._hs.bdim, self._hs.nbranch
+
+    def set_policies(self, rows, mask=None):
+        self._hs.set_policies(rows)
+
+    def solve(self, x, z, xref):
+        type(self).solves += 1
+        return self._hs.solve(x, z, xref)
+
+    def tree(self):
+        return self._hs.tree()
+
+
+@pytest.fixture
+def host_device(monkeypatch):
+    import hostsim_lib
+    from bmpc import plan
+    monkeypatch.setattr(plan, "BatchPlan", _HostPlan)
+    monkeypatch.setattr(plan, "model_eval", lambda desc, rows, x, u, z, device=0: hostsim_lib.model_eval(desc, rows, x, u, z))
+    _HostPlan.solves = 0
+    yield
+
+
+def test_reference_main_quadruped_runs_unchanged(host_device, monkeypatch):
+    """main_quadruped.py (reference :1-48): Quad_constants from the star import (:31),
+    BranchMPCProx, quadruped_env.sim(mpc) (:43) -- the scene loop is shortened to 2 s."""
+    import quadruped_env
+    full = quadruped_env.sim
+    recs = []
+    monkeypatch.setattr(quadruped_env, "sim", lambda mpc: recs.append(full(mpc, T=2.0)))
+    ns = runpy.run_path(os.path.join(REF, "main_quadruped.py"), run_name="ref_main_quadruped")
+    ns["main"]()
+    assert _HostPlan.solves == 10
+    state_rec, input_rec, backup_rec, choice_rec, xPred_rec, zPred_rec = recs[0]
+    assert np.all(np.isfinite(state_rec)) and np.all(np.isfinite(input_rec))
+    # the ego moves under the MPC's inputs, bounded by Fu (vxm 0.2, vym 0.1, rm 0.5)
+    assert np.all(np.abs(input_rec[0][:, 0]) <= 0.2 + 1e-6) and np.all(np.abs(input_rec[0][:, 2]) <= 0.5 + 1e-6)
+    assert len(xPred_rec[0]) == 6        # BT2array over the 2 + 4 non-root branches
+
+
+def test_reference_main_branch_runs_unchanged(host_device, monkeypatch):
+    """main_branch.sim_overtake (reference :20-51): BranchMPC_CVaR with N=8, NB=2 in the
+    overtake scene (Highway_env_branch.sim_overtake) -- shortened to 1 s."""
+    import Highway_env_branch
+    full_sim = Highway_env_branch.Highway_sim
+    recs = []
+
+    def short(env, T):
+        recs.append(full_sim(env, 1.0))
+        return recs[-1]
+    monkeypatch.setattr(Highway_env_branch, "Highway_sim", short)
+    ns = runpy.run_path(os.path.join(REF, "main_branch.py"), run_name="ref_main_branch")
+    ns["sim_overtake"]()
+    assert _HostPlan.solves == 10
+    state_rec, input_rec = recs[0][0], recs[0][1]
+    assert np.all(np.isfinite(state_rec))
+    assert np.all(np.abs(input_rec[0][:, 1]) <= 0.3 + 1e-6)     # steering-rate bound rm
+
+
+def test_bt_is_live_after_solve(host_device):
+    """mpc.BT is populated after every solve (reference keeps a live BranchTree)."""
+    import Init_MPC
+    import MPC_branch
+    from highway_branch_dyn import PredictiveModel, backup_brake, backup_lc, backup_maintain
+    from utils import Branch_constants
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=6.0, rm=0.3, J_c=20, s_c=1,
+                            ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    xRef = np.array([0.5, 1.8, 15, 0])
+    model = PredictiveModel(4, 2, 8, [lambda x: backup_maintain(x, cons), lambda x: backup_brake(x, cons),
+                                      lambda x: backup_lc(x, xRef)], 0.1, cons)
+    mpc = MPC_branch.BranchMPC_CVaR(Init_MPC.initBranchMPC(4, 2, 8, 2, xRef, 6.0, 0.3, 4, cons.W), model, 0.9)
+    assert mpc.BT is None
+    mpc.solve(np.array([0, 1.8, 20, 0.]), np.array([5, 5.4, 20, 0.]), xRef)
+    bt = mpc.BT
+    assert bt is not None and len(bt.children) == 3 and len(bt.children[0].children) == 3
+    w = sum(c.w for c in bt.children)
+    assert abs(w - 1.0) < 1e-12
+    assert bt.children[1].xtraj.shape == (8, 4)
+    first = mpc.BT
+    mpc.solve(np.array([2, 1.8, 20, 0.]), np.array([7, 5.4, 20, 0.]), xRef)
+    assert mpc.BT is not first              # rebuilt for the new solve
