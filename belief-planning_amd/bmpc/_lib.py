@@ -34,12 +34,16 @@ def headers():
 
 def build(force: bool = False, verbose: bool = False, profile: bool = False) -> str:
     """Compile libbmpc.so (or the phase-counter variant libbmpc_prof.so) for gfx950 in-tree
-    if missing or stale."""
+    unless a build of exactly these sources exists: the sidecar ``<so>.srchash`` records the
+    source_hash() a library was compiled from (an mtime check would accept a stale binary
+    that merely carries a newer timestamp)."""
     out = PROF_SO_PATH if profile else SO_PATH
-    if not force and os.path.exists(out):
-        newest = max(os.path.getmtime(p) for p in sources() + headers())
-        if os.path.getmtime(out) >= newest:
-            return out
+    stamp = out + ".srchash"
+    want = source_hash()
+    if not force and os.path.exists(out) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == want:
+                return out
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
            *(["-DBMPC_PROFILE"] if profile else []),
@@ -48,6 +52,8 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False) -> 
         print(" ".join(cmd))
     subprocess.check_call(cmd)
     os.replace(out + ".tmp", out)
+    with open(stamp, "w") as f:
+        f.write(want + "\n")
     return out
 
 
@@ -107,3 +113,15 @@ def check(rc: int, what: str):
         msg = lib().bmpc_last_error().decode(errors="replace")
         raise BmpcUnavailable(f"{what} failed ({rc}): {msg}") if rc in (-19, -5, -12) else RuntimeError(
             f"{what} failed ({rc}): {msg}")
+
+
+def source_hash() -> str:
+    """sha1 over the kernel sources and the ABI header: ties a profile (e.g. the PMC traffic
+    bench.py reports) to the build it was measured on."""
+    import hashlib
+    h = hashlib.sha1()
+    for p in sorted(sources() + headers()):
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode())
+            h.update(f.read())
+    return h.hexdigest()[:16]

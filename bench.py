@@ -24,6 +24,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "branch-MPC solves/sec (whole node), highway N=20 M=3 branches, batch 4096 egos"
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector (= FP64 matrix) peak, spec
+HBM_PEAK_TBPS = 8.0         # MI355X HBM3E peak, spec (MI355X_MICROARCH.md)
 
 
 def flops_per_iter(T, n, d, Nc, nFu, cone_dims):
@@ -39,41 +40,66 @@ def flops_model(U, Bn, bdim, m, N, n):
     return (U + Bn) * 40 + bdim * (m * N * 60 + (2 * N * m * 50) * (1 + n)) + U * 30
 
 
-def cpu_baseline(N, NB, sample, procs):
-    """Oracle (NumPy restatement of the reference + ECOS-algorithm IPM) on host cores."""
-    import multiprocessing as mp
-    t0 = time.time()
-    with mp.get_context("spawn").Pool(procs, initializer=_worker_init) as pool:
-        res = pool.map(_cpu_solve, [(i, N, NB) for i in range(sample)])
-    dt = time.time() - t0
-    return dict(value=sample / dt, unit="solves/s", cores=procs, kind="port",
-                sample=f"{sample} first solves of seeded egos (seed 0) at N={N} NB={NB} m=3, "
-                       f"oracle/ (NumPy model+tree assembly, ECOS-algorithm IPM with sparse LU), "
-                       f"{procs} processes x 1 thread, {dt:.1f} s wall incl. pool start",
-                per_solve_s=float(np.mean([r for r in res])))
+def usable_cores():
+    """Host cores this process may use: the affinity mask, capped by the cgroup CPU quota
+    and by OMP_NUM_THREADS when set (the GPU box grants a 16-CPU share of a larger host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = min(v for v in (aff, quota, int(env) if env and env.isdigit() else None) if v)
+    return n, aff, quota
 
 
-def cpu_cxx_baseline(N, NB, sample, threads):
-    """The kernel's own algorithm compiled for the host (tests/hostsim, g++ -O2 -fopenmp),
-    OpenMP over `threads` host cores: SURVEY 8(d) CPU baseline (ii).  Two closed-loop steps
-    (cold + warm) of the first `sample` egos of the seeded population."""
+def cpu_cxx_baseline(N, NB, egos, warm_steps, threads):
+    """SURVEY 8(d) CPU baseline (ii): the kernel algorithm compiled for the host
+    (tests/hostsim, g++ -O2 -fopenmp), OpenMP over `threads` cores, steady state: one cold
+    closed-loop step (inittree, untimed), then `warm_steps` timed warm steps (updatetree +
+    IPM) of `egos` seeded egos, with the same device-scene rules stepped by the host build."""
     os.environ["OMP_NUM_THREADS"] = str(threads)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import hostsim_lib as H
+    from bmpc import abi
     from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch
-    x, z, xref, tgt = seeded_batch(sample, seed=0)
-    hs = H.HostSim(highway_desc(N=N, NB=NB), sample)
+    x, z, xref, tgt = seeded_batch(egos, seed=0)
+    hs = H.HostSim(highway_desc(N=N, NB=NB), egos)
     hs.set_policies(highway_policy_rows(tgt))
+    env = abi.make_env()
+    scene = np.zeros((egos, abi.ENV_STRIDE))
+    scene[:, 0:4], scene[:, 4:8] = x, z
+    x, z, xref = hs.env_step(env, 0, scene)
+    r = hs.solve(x, z, xref)                        # cold solve (untimed)
     t0 = time.time()
-    for _ in range(2):
+    for t in range(1, warm_steps + 1):
+        x, z, xref = hs.env_step(env, t, scene, r["upred"], r["J"], r["status"], r["iters"])
         r = hs.solve(x, z, xref)
-        u0 = r["upred"][:, 0]
-        x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
-        z = z + 0.1 * np.stack([z[:, 2] * np.cos(z[:, 3]), z[:, 2] * np.sin(z[:, 3]), 0 * z[:, 0], 0 * z[:, 0]], 1)
     dt = time.time() - t0
-    return dict(value=round(2 * sample / dt, 2), unit="solves/s", cores=threads, kind="port",
-                sample=f"{sample} seeded egos x 2 closed-loop steps (cold + warm), the kernel algorithm built "
-                       f"for the host (g++ -O2 -fopenmp, {threads} threads), {dt:.1f} s")
+    return dict(value=round(warm_steps * egos / dt, 2), unit="solves/s", cores=threads, kind="port",
+                sample=f"{egos} seeded egos x {warm_steps} warm closed-loop steps after one untimed cold step, "
+                       f"N={N} NB={NB}: the kernel algorithm built for the host from the same csrc templates "
+                       f"(tests/hostsim, g++ -O2 -fopenmp, {threads} OpenMP threads), {dt:.2f} s wall")
+
+
+def cpu_oracle_baseline(N, NB, egos, warm_steps, procs):
+    """The NumPy oracle (reference-structured: model + tree assembly + ECOS-algorithm IPM),
+    one process per core, steady state: per ego one untimed cold solve then `warm_steps`
+    timed warm solves along the closed loop."""
+    import multiprocessing as mp
+    t0 = time.time()
+    with mp.get_context("spawn").Pool(procs, initializer=_worker_init) as pool:
+        res = pool.map(_oracle_episode, [(i, N, NB, warm_steps) for i in range(egos)])
+    wall = time.time() - t0
+    per = float(np.mean([r for rs in res for r in rs]))
+    return dict(value=round(procs / per, 3), unit="solves/s", cores=procs, kind="port",
+                sample=f"{egos} seeded egos x {warm_steps} warm solves (after one untimed cold solve each), N={N} "
+                       f"NB={NB}: oracle/ (NumPy model + tree assembly + ECOS-algorithm IPM), {procs} processes x 1 "
+                       f"thread; value = procs / mean warm-solve time ({per:.3f} s), {wall:.1f} s wall incl. pool start")
 
 
 def _worker_init():
@@ -84,76 +110,119 @@ def _worker_init():
             sys.path.insert(0, _p)
 
 
-def _cpu_solve(args):
-    i, N, NB = args
+def _oracle_episode(args):
+    i, N, NB, warm = args
     from bmpc.scenarios import seeded_batch
     from oracle.ecos_ipm import ecos_solve
     from oracle.model import HighwayModel, highway_policies
     from oracle.tree import CVaRController
     x, z, xref, tgt = seeded_batch(max(i + 1, 2), seed=0)
+    x, z, xr = x[i].copy(), z[i].copy(), xref[i].copy()
     mdl = HighwayModel(N, 0.1, highway_policies(0.1, tgt[i]))
     Fx = np.array([[0., 1, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1], [0, 0, 0, -1]])
     c = CVaRController(mdl, N, NB, np.diag([0., 3, 3, 10]), np.diag([1., 100]), Fx,
                        [4 * 3.6 - 1.25, -1.25, .25, .25], np.kron(np.eye(2), [1, -1]).T,
-                       [6., 6., .3, .3], [0, 300], xref[i], 0.9, solver=ecos_solve)
-    t0 = time.time()
-    c.solve(x[i], z[i], xref[i])
-    return time.time() - t0
+                       [6., 6., .3, .3], [0, 300], xr, 0.9, solver=ecos_solve)
+    times = []
+    for k in range(warm + 1):
+        t0 = time.time()
+        c.solve(x, z, xr)
+        if k > 0:
+            times.append(time.time() - t0)
+        u = c.uPred[0]
+        x = x + 0.1 * np.array([x[2] * np.cos(x[3]), x[2] * np.sin(x[3]), u[0], u[1]])
+        z = z + 0.1 * np.array([z[2] * np.cos(z[3]), z[2] * np.sin(z[3]), 0.0, 0.0])
+    return times
 
 
-def load_traffic(path):
-    """Per-launch HBM bytes of the IPM kernel from a committed rocprofv3 --pmc summary."""
+def load_traffic(path, key, src):
+    """Per-launch HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes) of the IPM
+    kernel, measured for THIS workload key on THIS source build (profiles/pmc_traffic.json,
+    written by tools/prof_summary.py); None when no entry matches."""
     if not path or not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get("k_ipm_bytes_per_launch")
-    except Exception:
-        return None
+            entries = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for e in entries:
+        if e.get("key") == key and e.get("source_hash") == src:
+            return e.get("bytes_per_launch"), e.get("profile")
+    return None, None
+
+
+def algorithmic_bytes(T, U, bdim, nbranch, m, n, d):
+    """SURVEY 8(d) compulsory HBM bytes per solve: inputs 3n, warm start read + write
+    2[(U+1)d + bdim m + d], outputs U d + T n + Bn + 2 (J, status)."""
+    return 8 * (3 * n + 2 * ((U + 1) * d + bdim * m + d) + U * d + T * n + (nbranch - 1) + 2)
+
+
+def launch_ranks(a):
+    """bench.py --gpus N run directly: start N ranks through torchrun (127.0.0.1) as child
+    processes before this process touches the GPU, and exit with their status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")))
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); run directly with N > 1 it "
+                                                        "launches the ranks itself through torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("highway", "quadruped", "robust"), default="highway",
                     help="highway = BASELINE metric config; quadruped = BASELINE config 4 (BranchMPCProx)")
     ap.add_argument("--batch", type=int, default=None, help="egos per GPU (highway 4096, quadruped 1024)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="egos over all ranks, sharded contiguously (BASELINE config 5: 65536 over 8 GPUs)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--NB", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=24)
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--cpu-egos", type=int, default=4096, help="egos of the C++ host-build baseline sample")
+    ap.add_argument("--oracle-egos", type=int, default=16, help="egos of the NumPy-oracle baseline sample")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(a)                 # never returns
     quad = a.workload == "quadruped"
     robust = a.workload == "robust"     # robustMPC (MPC_branch.py:1275) in the same scene
-    a.batch = a.batch or (1024 if quad else 4096)
     a.N = a.N or (25 if quad else 20)
     a.NB = a.NB or (2 if quad else 1)
 
     import torch
     import torch.distributed as dist
-    from bmpc import abi, plan
+    from bmpc import _lib, abi, plan
     from bmpc.scenarios import (highway_desc, highway_policy_rows, quadruped_desc, quadruped_policy_rows,
                                 seeded_batch, seeded_quadruped_batch)
 
     from bmpc import distributed as D
     rank, local, world = D.world()
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     D.init("nccl", device=dev)
-    B = a.batch
-    # one global seeded population of B*world egos (SURVEY §8(d)); rank r owns a contiguous shard
-    lo, hi = D.shard(B * world, rank, world)
+    if world > 1:
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+    # one global seeded population (SURVEY §8(d)); rank r owns a contiguous shard of it
+    G = a.global_batch or (a.batch or (1024 if quad else 4096)) * world
+    lo, hi = D.shard(G, rank, world)
+    B = hi - lo
     if quad:
-        x, z, xref = (v[lo:hi] for v in seeded_quadruped_batch(B * world, seed=1))
+        x, z, xref = (v[lo:hi] for v in seeded_quadruped_batch(G, seed=1))
         desc = quadruped_desc(N=a.N, NB=a.NB)
         pl = plan.BatchPlan(desc, B, device=local)
         pl.set_policies(quadruped_policy_rows(B))
     else:
-        x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(B * world, seed=0))
+        x, z, xref, tgt = (v[lo:hi] for v in seeded_batch(G, seed=0))
         desc = highway_desc(N=a.N, NB=a.NB)
         if robust:
             desc.controller = abi.CTRL_ROBUST
@@ -245,8 +314,9 @@ def main():
     elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
     tm = pl.timing()
     pl.enable_timing(False)
+    ipm_ms = D.max_over_ranks(tm["ipm_ms"], device=dev)
     iters_mean = float(it_sum.sum().item()) / (B * max(a.steps, 1))
-    total = B * world * a.steps
+    total = G * a.steps
     value = total / elapsed
     if rank == 0:
         st_h = stats.cpu().numpy()
@@ -261,8 +331,14 @@ def main():
             cone_dims = [2 + a.N * 6] * (bdim * 3) + [4]
             F_it = flops_per_iter(T, 4, 2, 5, 4, cone_dims)
             F_mod = flops_model(U, nbr - 1, bdim, 3, a.N, 4)
-        achieved = B * iters_mean * F_it / (tm["ipm_ms"] * 1e-3) / 1e12 if tm["ipm_ms"] > 0 else 0.0
-        traffic = None if (quad or robust) else load_traffic(a.traffic)
+        kern_s = ipm_ms * 1e-3
+        achieved = B * iters_mean * F_it / kern_s / 1e12 if kern_s > 0 else 0.0
+        abytes = algorithmic_bytes(T, U, bdim, nbr, desc.m, desc.n, desc.d)
+        hbm_alg = B * abytes / kern_s / 1e9 if kern_s > 0 else 0.0
+        key = f"{a.workload}:N{a.N}:NB{a.NB}:B{B}"
+        src = _lib.source_hash()
+        traffic, tsrc = load_traffic(a.traffic, key, src)
+        kname = "k_qp (structured Mehrotra QP IPM)" if (quad or robust) else "k_ipm (structured HSDE IPM)"
         out = {
             "metric": (METRIC if not (quad or robust) else
                        "branch-MPC solves/sec (whole node), quadruped BranchMPCProx N=25 NB=2 m=2 (4 leaves), "
@@ -271,20 +347,23 @@ def main():
                        f"predictions per slot, batch {B} egos"),
             "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak" if not a.global_batch else "strong",
+            "vs_baseline": None, "dtype": "f64",
             "data": ("synthetic (seeded quadruped egos, seed 1; obstacle on the forward policy)" if quad
                      else "synthetic (seeded SURVEY §8d egos, sim_overtake row 0)"),
             "config": {"workload": (f"quadruped BranchMPCProx closed loop, N={a.N}, NB={a.NB}, m=2 " if quad else
                                     f"highway robustMPC closed loop, N={a.N}, NB={a.NB}, m=3 " if robust else
                                     f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
                                    + f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"ego-sharded dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
+                       "global_batch": G, "world_size": world, "parallelism": f"ego-sharded dp{world}"},
+            "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
-                         "traffic": traffic,
-                         "kernel": "k_qp (structured Mehrotra QP IPM)" if (quad or robust) else
-                                   "k_ipm (structured HSDE IPM)",
-                         "kernel_ms": round(tm["ipm_ms"], 4),
+                         "traffic": traffic, "traffic_source": tsrc, "traffic_key": key, "source_hash": src,
+                         "hbm_alg_GBps": round(hbm_alg, 4), "hbm_frac": round(hbm_alg / (HBM_PEAK_TBPS * 1e3), 9),
+                         "alg_bytes_per_solve": abytes,
+                         "hbm_traffic_frac": (round(traffic / kern_s / (HBM_PEAK_TBPS * 1e12), 4)
+                                              if traffic and kern_s > 0 else None),
+                         "kernel": kname, "kernel_ms": round(ipm_ms, 4),
                          "tree_kernel_ms": round(tm["tree_ms"], 4),
                          "flop_per_iter": F_it, "iters_mean": round(iters_mean, 2),
                          "flop_model_per_solve": F_mod},
@@ -296,13 +375,15 @@ def main():
                             "env": "device k_env (sim_overtake scene)" if not quad else "torch ops"},
         }
         if not a.no_cpu_baseline and world == 1 and not (quad or robust):
-            procs = max(1, min(8, len(os.sched_getaffinity(0))))
-            cb = cpu_baseline(a.N, a.NB, a.cpu_sample, procs)
-            out["cpu_baseline"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in cb.items()}
+            cores, aff, quota = usable_cores()
             try:
-                out["cpu_cxx_baseline"] = cpu_cxx_baseline(a.N, a.NB, 1024, max(1, min(16, len(os.sched_getaffinity(0)))))
-            except Exception as exc:   # the C++ host build is a secondary figure only
-                out["cpu_cxx_baseline"] = {"error": str(exc)[:200]}
+                cb = cpu_cxx_baseline(a.N, a.NB, min(a.cpu_egos, G), 3, cores)
+            except Exception as exc:
+                cb = {"error": str(exc)[:200]}
+            cb["affinity_cpus"], cb["cgroup_quota_cpus"] = aff, quota
+            out["cpu_baseline"] = cb
+            ob = cpu_oracle_baseline(a.N, a.NB, a.oracle_egos, 2, cores)
+            out["cpu_oracle_baseline"] = ob
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

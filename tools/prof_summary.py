@@ -71,11 +71,23 @@ def main(out):
                   "hbm_GBps": byt / dur if dur else None}
             with open(os.path.join(out, f"{k}_pmc_traffic.json"), "w") as f:
                 json.dump(tj, f, indent=1)
+            if KEY:   # entry for profiles/pmc_traffic.json (bench.py looks it up by key + source hash)
+                sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                "belief-planning_amd"))
+                from bmpc import _lib
+                ent = {"key": KEY, "source_hash": _lib.source_hash(), "kernel": k, "bytes_per_launch": byt,
+                       "fetch_kB": fk, "write_kB": wk, "avg_dispatch_ns": dur,
+                       "profile": os.path.basename(out) + " (rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE; "
+                                  "bytes = 2 x FETCH_SIZE + WRITE_SIZE)"}
+                with open(os.path.join(out, "pmc_entry.json"), "w") as f:
+                    json.dump(ent, f, indent=1)
     for d in ("stats", "fetch", "write", "sq", "tcc"):
         shutil.rmtree(os.path.join(out, d), ignore_errors=True)
     print(json.dumps(summ.get("kernel_durations_ns", {}), indent=1))
     print(json.dumps(agg, indent=1))
 
+
+KEY = sys.argv[2] if len(sys.argv) > 2 else None
 
 if __name__ == "__main__":
     main(sys.argv[1])
