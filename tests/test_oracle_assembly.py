@@ -78,8 +78,12 @@ def test_oracle_ipm_certifies_reference_problems(name):
         x, info = ecos_solve(prob)
         assert info["exitFlag"] in (0, 10)
         r = kkt_residuals(prob, info["x"], info["y"], info["z"], info["s"])
-        assert r["eq"] < 1e-9 and r["ineq"] < 1e-7 and r["dual"] < 1e-5 and r["cone"] > -1e-6
-        assert abs(r["pcost"] - r["dcost"]) <= 1e-6 * max(1.0, abs(r["pcost"]))
+        if info["exitFlag"] == 0:      # ECOS full accuracy (feastol = abstol = reltol = 1e-8)
+            assert r["eq"] < 1e-9 and r["ineq"] < 1e-7 and r["dual"] < 1e-5 and r["cone"] > -1e-6
+            assert abs(r["pcost"] - r["dcost"]) <= 1e-6 * max(1.0, abs(r["pcost"]))
+        else:                          # ECOS "inaccurate" (feastol 1e-4, abstol / reltol 5e-5)
+            assert r["eq"] < 1e-9 and r["ineq"] < 1e-5 and r["dual"] < 1e-4 and r["cone"] > -1e-5
+            assert abs(r["pcost"] - r["dcost"]) <= 5e-5 * max(1.0, abs(r["pcost"]))
         assert abs(x[-1] - g[f"s{t}_sol"][-1]) <= 1e-9 * max(1, abs(x[-1]))
 
 

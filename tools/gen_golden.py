@@ -9,10 +9,12 @@ solver packages they name are replaced by import stubs (SURVEY §8c route 1):
   ECOS-algorithm restatement (``oracle/ecos_ipm.py``);
 * ``osqp``   -- likewise for ``OSQP.setup/solve`` (quadruped ``BranchMPCProx``).
 
-The predictive model handed to the reference controller is the oracle's NumPy
-restatement of the CasADi graphs (CasADi is absent).  So the *tree bookkeeping, warm
-start, linearisation schedule and problem assembly* in the fixtures are produced by the
-reference code itself; model values come from the oracle; solutions from the oracle IPM.
+The predictive model handed to the reference controller is the reference's OWN
+``highway_branch_dyn`` / ``quadruped_branch_dyn`` ``PredictiveModel``, built over the CasADi
+API stand-in ``tools/casadi_shim`` (CasADi is absent; ``tools/gen_golden_model.py``).  So
+the *model values, tree bookkeeping, warm start, linearisation schedule and problem
+assembly* in the fixtures are produced by the reference code itself; the solutions come
+from the oracle's ECOS-algorithm / QP interior points behind the solver stubs.
 
 Outputs ``tests/golden/*.npz`` (data only, no reference source).  Usage:
     python tools/gen_golden.py [--quick]
@@ -32,6 +34,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 REF = "/root/reference"
 sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
 
 from oracle import ecos_ipm, qp_ipm  # noqa: E402
 from oracle.env import HighwayOvertake  # noqa: E402
@@ -39,6 +42,46 @@ from oracle.model import HighwayModel, QuadrupedModel, highway_policies, quadrup
 from oracle.tree import ConeProblem, QPProblem  # noqa: E402
 
 CURRENT = {}
+REFMOD = {}
+
+
+def ref_models():
+    """The reference's highway / quadruped model modules over the CasADi shim."""
+    if not REFMOD:
+        from gen_golden_model import import_reference_models
+        H, Q, _, _ = import_reference_models()
+        REFMOD.update(H=H, Q=Q)
+    return REFMOD["H"], REFMOD["Q"]
+
+
+class RefHighwayModel:
+    """The reference's ``highway_branch_dyn.PredictiveModel`` (its own lambdas and graphs)
+    behind the oracle env's ``update_backup(policy list)`` call: the lane-change target of
+    the oracle's third policy is re-issued as the reference's ``backup_lc`` lambda
+    (``Highway_env_branch.py:117-118``)."""
+
+    def __init__(self, N, dt, cons, lc_target):
+        self.H, _ = ref_models()
+        self.cons = cons
+        self.inner = self.H.PredictiveModel(4, 2, N, self._lambdas(lc_target), dt, cons)
+
+    def _lambdas(self, tgt):
+        H, cons, t = self.H, self.cons, np.array(tgt, float)
+        return [lambda x: H.backup_maintain(x, cons), lambda x: H.backup_brake(x, cons), lambda x: H.backup_lc(x, t)]
+
+    def update_backup(self, policies):
+        self.inner.update_backup(self._lambdas(policies[2].params))
+
+    def __getattr__(self, k):
+        return getattr(self.inner, k)
+
+
+def ref_quadruped_model(N, dt, v0, L1, W1, L2, W2, col_tol):
+    _, Q = ref_models()
+    import utils
+    cons = utils.Quad_constants(s1=2, s2=3, c2=0.5, alpha=1, R=1.2, vxm=0.2, vym=0.1, rm=0.5, L1=L1, W1=W1, L2=L2,
+                                W2=W2, col_tol=col_tol, col_alpha=5)
+    return Q.PredictiveModel(3, 3, N, [lambda x: Q.backup_forward(x, v0), lambda x: Q.backup_stop(x)], dt, cons)
 
 
 def install_stubs():
@@ -126,7 +169,7 @@ def gen_highway(name, N, NB, steps, keep, out):
     xRef0 = np.array([0.5, 1.8, 15, 0])
     cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
                             s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
-    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    model = RefHighwayModel(N, dt, cons, xRef0)
     param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
     mpc = MPC_branch.BranchMPC_CVaR(param, model, ralpha=0.9)
     CURRENT["mpc"] = mpc
@@ -198,7 +241,7 @@ def gen_highway_qp(name, N, NB, steps, keep, out):
     xRef0 = np.array([0.5, 1.8, 15, 0])
     cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
                             s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
-    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    model = RefHighwayModel(N, dt, cons, xRef0)
     param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
     mpc = MPC_branch.BranchMPC(param, model)
     CURRENT["mpc"] = mpc
@@ -253,7 +296,7 @@ def gen_highway_robust(name, N, NB, steps, keep, out):
     xRef0 = np.array([0.5, 1.8, 15, 0])
     cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
                             s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
-    model = HighwayModel(N, dt, highway_policies(cons.Kpsi, xRef0), L=cons.L, W=cons.W, s1=cons.s1)
+    model = RefHighwayModel(N, dt, cons, xRef0)
     param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
     mpc = MPC_branch.robustMPC(param, model)
     CURRENT["mpc"] = mpc
@@ -307,7 +350,7 @@ def gen_quadruped(name, steps, keep, out):
     vxm, vym, rm, v0 = 0.2, 0.1, 0.5, 0.2
     L1, L2, W1, W2, col_tol = 0.5, 1.0, 0.3, 0.6, 0.2
     xRef = np.array([5., 5., 0.])
-    model = QuadrupedModel(N, dt, quadruped_policies(v0), L1=L1, W1=W1, L2=L2, W2=W2, col_tol=col_tol, s1=2.0)
+    model = ref_quadruped_model(N, dt, v0, L1, W1, L2, W2, col_tol)
     param = Init_MPC.initquadBranchMPC(n, d, N, NB, xRef, vxm, vym, rm)
     mpc = MPC_branch.BranchMPCProx(param, model)
     CURRENT["mpc"] = mpc
