@@ -70,34 +70,30 @@ BMPC_HD T* uniform_ptr(T* p) {
 // ------------------------------------------------------------------------------------
 // Plan: per-plan constants and topology tables (shared by every ego of the batch).
 // ------------------------------------------------------------------------------------
-struct Topo {
-  // per branch (BFS order of MPC_branch.inittree)
-  gint* br_depth;
-  gint* br_len;
-  gint* br_ndx;
-  gint* br_ndu;
-  gint* br_child0;   // first child (children are contiguous), -1 for leaves
-  // per x node
-  gint* x_u;         // u node of x node (-1 for leaf terminal nodes)
-  gint* x_srcu;      // u node whose (A,B,C) defines this node (-1 for root)
-  gint* x_srcx;      // x node of that source
-  gint* x_cone;      // cone whose middle rows contain x (-1 none)
-  gint* x_conepos;   // position j of the node inside the cone's branch
-  gint* x_branch;
-  gint* succ_off;    // CSR successors of each x node: nodes defined by its (A,B,C)
-  gint* succ;
-  gint* lvl_off;     // x nodes grouped by tree level (root = level 0)
-  gint* lvl_nodes;
-  // per u node
-  gint* u_x;
-  gint* u_cone;
-  // per cone
-  gint* cone_b;      // parent non-leaf branch index (-1 = root cone)
-  gint* cone_i;      // child slot i
-  gint* cone_c;      // child branch (-1 = root cone)
-  gint* cone_q;      // cone dimension
-  gint* cone_off;    // first row of the cone in the conic row vector
+// The tables (one concatenated int32 blob, see HostPlan): per branch in BFS order of
+// MPC_branch.inittree -- depth, length, first x / u node, first child (children are
+// contiguous; -1 for leaves); per x node -- its u node (-1 for leaf terminal nodes), the
+// u node whose (A,B,C) defines it and that node's x (-1 for the root), the cone whose middle
+// rows contain it (-1 none) and its position in that cone's branch, its branch, CSR
+// successors (nodes defined by its (A,B,C)), the nodes grouped by tree level; per u node --
+// its x node and cone; per cone -- parent non-leaf branch (-1 = root cone), child slot,
+// child branch (-1 = root cone), dimension and first row in the conic row vector.
+#define BMPC_TOPO_FIELDS(F)                                                                  \
+  F(br_depth) F(br_len) F(br_ndx) F(br_ndu) F(br_child0) F(x_u) F(x_srcu) F(x_srcx) F(x_cone) \
+  F(x_conepos) F(x_branch) F(succ_off) F(succ) F(lvl_off) F(lvl_nodes) F(u_x) F(u_cone)       \
+  F(cone_b) F(cone_i) F(cone_c) F(cone_q) F(cone_off)
+#define BMPC_TOPO_COUNT_(n) +1
+enum { BMPC_TOPO_N = 0 BMPC_TOPO_FIELDS(BMPC_TOPO_COUNT_) };
+#define BMPC_TOPO_MEMBER_(n) IP n;
+template <class IP>
+struct TopoT {
+  BMPC_TOPO_FIELDS(BMPC_TOPO_MEMBER_)
 };
+// the tables in global memory (k_tree) and the per-wave LDS copy (k_ipm / k_qp: every
+// topology lookup on the solver's dependent chains is an LDS read, not a memory round trip)
+typedef const BMPC_AS_LDS int32_t lint;
+typedef TopoT<gint*> Topo;
+typedef TopoT<lint*> TopoL;
 
 struct Plan {
   bmpc_plan_desc desc;
@@ -124,7 +120,19 @@ struct Plan {
   double QQ[BMPC_MAX_N * BMPC_MAX_N];   // W1'W1
   double RR[BMPC_MAX_D * BMPC_MAX_D];   // Wu'Wu
   Topo t;
+  int toff[BMPC_TOPO_N];   // offset of each table in the blob (int32 units)
+  int ntab;                // blob length (int32 units); its LDS copy follows the nlds doubles
 };
+
+// LDS view of the topology tables (ex.tab = the wave's copy of the blob)
+#define BMPC_TOPO_SET_(n) v.n = ex.tab + P.toff[i++];
+template <class X>
+BMPC_HD TopoL topo_view(const BMPC_AS_CONST Plan& P, const X& ex) {
+  TopoL v;
+  int i = 0;
+  BMPC_TOPO_FIELDS(BMPC_TOPO_SET_)
+  return v;
+}
 
 // ------------------------------------------------------------------------------------
 // Per-ego workspace layout (offsets in doubles inside one ego's slab)

@@ -36,7 +36,8 @@ __device__ __forceinline__ double dpp_d(double v) {
 
 struct DevExec {
   int lane;
-  ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm only)
+  ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm / k_qp only)
+  lint* tab;     // this wave's LDS copy of the topology tables (k_ipm / k_qp only)
   static constexpr int nlanes = 64;
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
@@ -83,6 +84,17 @@ struct Bundle {
   Layout L;
 };
 
+// Dynamic LDS of the solver kernels: Plan::nlds doubles of scratch, then a copy of the
+// topology tables (Plan::ntab int32).  The copy is one batched pass at kernel start; every
+// later tree / cone / node-index lookup of the solve is an LDS read.
+__device__ __forceinline__ DevExec solver_exec(const Plan& P, double* lds_dyn) {
+  int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
+  const int32_t* gtab = (const int32_t*)P.t.br_depth;   // blob base (the first table)
+  for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];
+  __syncthreads();
+  return DevExec{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl};
+}
+
 template <class M>
 __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
                                              const bmpc_policy* __restrict__ pol,
@@ -92,7 +104,7 @@ __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, doubl
   if (e >= batch) return;
   const Plan& P = B->P;
   const Layout& L = B->L;
-  DevExec ex{(int)threadIdx.x, nullptr};
+  DevExec ex{(int)threadIdx.x, nullptr, nullptr};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   BMPC_PROF(E.ws, L, PROF_TREE);
   tree_step<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
@@ -108,7 +120,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  DevExec ex{(int)threadIdx.x, (ldouble*)lds_dyn};
+  const DevExec ex = solver_exec(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_ipm<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -135,7 +147,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  DevExec ex{(int)threadIdx.x, (ldouble*)lds_dyn};
+  const DevExec ex = solver_exec(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_qp<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -427,7 +439,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
-  size_t lds_bytes = sizeof(double) * (size_t)P.nlds;
+  size_t lds_bytes = sizeof(double) * (size_t)P.nlds + ((sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
   if (const char* e = getenv("BMPC_IPM_LDS_BYTES")) {

@@ -90,12 +90,13 @@ BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
 
 // cone-group rounds (see ConeGroups): G, and per round k / off / q of the owned cone
 #define BMPC_CONE_ROUNDS(ex, P, G)                                \
+  const TopoL G##_t = topo_view((P), ex);                         \
   const ConeGroups G = cone_groups(ex, (P).cgrp, (P).ncones);     \
   for (int rnd_ = 0; rnd_ < G.rounds; ++rnd_)
 #define BMPC_CONE_K(P, G, k, off, q)                              \
   const int k = rnd_ * G.ngrp + G.g < (P).ncones ? rnd_ * G.ngrp + G.g : -1; \
-  const int off = k >= 0 ? (P).t.cone_off[k] : 0;                 \
-  const int q = k >= 0 ? (P).t.cone_q[k] : 0
+  const int off = k >= 0 ? G##_t.cone_off[k] : 0;                 \
+  const int q = k >= 0 ? G##_t.cone_q[k] : 0
 
 // ------------------------------------------------------------------------------------
 // block of dot products in one pass: acc[a][b] = sum_i A_a[i] B_b[i] over the tree-variable
@@ -178,7 +179,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
   BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
   BMPC_COUNT(C.ws, *C.L, PROF_NAPPLYG);
   BMPC_TIC(t_glp);
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.at(C.L->dh);
   // Fx rows + positivity rows
@@ -290,7 +291,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
   ctx_qx<NX>(C, qx);
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYGT);
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* boost = C.at(C.L->boost);
   const gdouble* dh = C.at(C.L->dh);
@@ -389,7 +390,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
 template <class X, int NX, int NU>
 BMPC_HD void apply_A(const X ex, const Ctx& C, const gdouble* zv, gdouble* out) {
   CPlan& P = *C.P;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const gdouble* Ad = C.at(C.L->Ad);
   const gdouble* Bd = C.at(C.L->Bd);
   struct V4 { double v[NX]; };
@@ -430,7 +431,7 @@ BMPC_HD void apply_A(const X ex, const Ctx& C, const gdouble* zv, gdouble* out) 
 template <class X, int NX, int NU>
 BMPC_HD void apply_AT(const X ex, const Ctx& C, const gdouble* y, gdouble* out) {
   CPlan& P = *C.P;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const gdouble* Ad = C.at(C.L->Ad);
   const gdouble* Bd = C.at(C.L->Bd);
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -489,7 +490,7 @@ BMPC_HD void apply_AT(const X ex, const Ctx& C, const gdouble* y, gdouble* out) 
 template <class X, int NX, int NU>
 BMPC_HD void build_hb(const X ex, const Ctx& C, gdouble* h, gdouble* bv) {
   CPlan& P = *C.P;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* h0 = C.at(C.L->h0);
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
@@ -594,8 +595,8 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   lane_batch(ex, c0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { wb[i] = v; vn[i] = v; });
   ex.sync();
   for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
-    wb[P.t.cone_off[k]] = 1.0;
-    vn[P.t.cone_off[k]] = 1.0;
+    wb[topo_view(P, ex).cone_off[k]] = 1.0;
+    vn[topo_view(P, ex).cone_off[k]] = 1.0;
     C.ws[C.L->eta + k] = 1.0;
   }
   ex.sync();
@@ -845,7 +846,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
   CPlan& P = *C.P;
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_FACTOR);
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const gdouble* dl = ws + L.dl;
@@ -1060,7 +1061,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_TREESOLVE);
   BMPC_COUNT(C.ws, L, PROF_NTREE);
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   gdouble* lv_ = ws + L.lvec;   // [nr][T][NX]
@@ -1596,7 +1597,7 @@ BMPC_HD void bring2cone(const X ex, const Ctx& C, const gdouble* r, gdouble* s) 
   }
   lane_batch<16>(ex, 0, P.nrows, [&](int i) { return r[i]; }, [&](int i, double v) { s[i] = i < P.nlp ? v + 1.0 + alpha : v; });
   ex.sync();
-  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) s[P.t.cone_off[k]] = r[P.t.cone_off[k]] + 1.0 + alpha;
+  for (int k = ex.lane; k < P.ncones; k += ex.nlanes) s[topo_view(P, ex).cone_off[k]] = r[topo_view(P, ex).cone_off[k]] + 1.0 + alpha;
   ex.sync();
 }
 
@@ -1859,7 +1860,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
         return i < P.nlp ? v + (sigma * mu) : v;   // + sigma mu e on the LP rows
       }, [&](int i, double v) { ra[i] = v; });
       ex.sync();
-      for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[P.t.cone_off[k]] += sigma * mu;   // ... and cone heads
+      for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[topo_view(P, ex).cone_off[k]] += sigma * mu;   // ... and cone heads
       ex.sync();
       jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
       apply_W(ex, C, 0, ds, rb, -1.0, rz, eta1);               // eta1 rz - W xi

@@ -85,13 +85,11 @@ void weight_root(const double* M, int n, double* W) {
 }  // namespace
 
 void HostPlan::point_tables(const int32_t* base) {
-  gint** ptrs[] = {&plan.t.br_depth, &plan.t.br_len, &plan.t.br_ndx, &plan.t.br_ndu,
-                            &plan.t.br_child0, &plan.t.x_u, &plan.t.x_srcu, &plan.t.x_srcx,
-                            &plan.t.x_cone, &plan.t.x_conepos, &plan.t.x_branch, &plan.t.succ_off,
-                            &plan.t.succ, &plan.t.lvl_off, &plan.t.lvl_nodes, &plan.t.u_x,
-                            &plan.t.u_cone, &plan.t.cone_b, &plan.t.cone_i, &plan.t.cone_c,
-                            &plan.t.cone_q, &plan.t.cone_off};
-  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) *ptrs[i] = (gint*)(base + blob_off[i]);
+  size_t i = 0;
+#define BMPC_TOPO_POINT_(n) plan.t.n = (gint*)(base + blob_off[i]), plan.toff[i] = (int)blob_off[i], ++i;
+  BMPC_TOPO_FIELDS(BMPC_TOPO_POINT_)
+#undef BMPC_TOPO_POINT_
+  plan.ntab = (int)blob.size();
 }
 
 std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
@@ -329,11 +327,9 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
     }
 
   // ---- concatenated tables -------------------------------------------------------------------
-  std::vector<int32_t>* tabs[] = {&hp.br_depth, &hp.br_len, &hp.br_ndx, &hp.br_ndu, &hp.br_child0,
-                                  &hp.x_u, &hp.x_srcu, &hp.x_srcx, &hp.x_cone, &hp.x_conepos,
-                                  &hp.x_branch, &hp.succ_off, &hp.succ, &hp.lvl_off,
-                                  &hp.lvl_nodes, &hp.u_x, &hp.u_cone, &hp.cone_b, &hp.cone_i,
-                                  &hp.cone_c, &hp.cone_q, &hp.cone_off};
+#define BMPC_TOPO_HOSTVEC_(n) &hp.n,
+  std::vector<int32_t>* tabs[] = {BMPC_TOPO_FIELDS(BMPC_TOPO_HOSTVEC_)};   // same order as Topo
+#undef BMPC_TOPO_HOSTVEC_
   hp.blob.clear();
   hp.blob_off.clear();
   for (auto* v : tabs) {

@@ -24,7 +24,7 @@ struct QpCtx {
 };
 
 // u node whose input created x node k's state (the rate-cost predecessor of x_u[k]); -1 root
-BMPC_HD int qp_pred_u(CPlan& P, int u) { return P.t.x_srcu[P.t.u_x[u]]; }
+BMPC_HD int qp_pred_u(const TopoL& t, int u) { return t.x_srcu[t.u_x[u]]; }
 
 // coefficient j of inequality row c of state node k: Ncol collision rows (-dh) then the Fx rows
 template <int NX>
@@ -33,7 +33,7 @@ BMPC_HD double qp_row(CPlan& P, const gdouble* dh, int k, int c, int j) {
 }
 // rows of state node k are live: every node with an input, and robustMPC's terminal node
 // (its Fx rows carry slacks, MPC_branch.py:1470-1472); BranchMPC's leaf terminals are empty
-BMPC_HD bool qp_rows_on(CPlan& P, int k) { return P.t.x_u[k] >= 0 || P.desc.controller == BMPC_CTRL_ROBUST; }
+BMPC_HD bool qp_rows_on(CPlan& P, const TopoL& t, int k) { return t.x_u[k] >= 0 || P.desc.controller == BMPC_CTRL_ROBUST; }
 
 // ---- cost, rhs (buildCost / buildIneqConstr / buildEqConstr of the current tree) ----------
 template <class X, class M>
@@ -42,7 +42,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
   constexpr int NX = M::NX, NU = M::NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   gdouble* ws = C.ws;
   const int Nc = P.Nc;
   const gdouble* w = ws + L.w;
@@ -84,7 +84,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
       }
       q[P.oX + k * NX + c] = v;
     }
-    for (int c = 0; c < Nc; ++c) q[P.oS + k * Nc + c] = qp_rows_on(P, k) ? P.desc.Qslack[1] * wb : 0.0;
+    for (int c = 0; c < Nc; ++c) q[P.oS + k * Nc + c] = qp_rows_on(P, t, k) ? P.desc.Qslack[1] * wb : 0.0;
   }
   // input nodes: diagonal blocks (doubled), rate couplings with the predecessor, qu
   const auto R = P.desc.R;
@@ -117,7 +117,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
         for (int c = 0; c < NU; ++c) D[r][c] += dR[r > c ? r : c];
     gdouble* Hu = ws + L.hu + u * NU * NU;
     gdouble* O = ws + L.qo + u * NU * NU;
-    const int pu = qp_pred_u(P, u);
+    const int pu = qp_pred_u(t, u);
     for (int r = 0; r < NU; ++r)
       for (int c = 0; c < NU; ++c) {
         Hu[r * NU + c] = 2.0 * D[r][c];
@@ -133,7 +133,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
   const gdouble* h0 = ws + L.h0;
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
     const int k = it / Nc, c = it % Nc;
-    hv[P.rFx + it] = !qp_rows_on(P, k) ? 0.0 : c < P.Ncol ? h0[k * P.Ncol + c] : P.desc.bx[c - P.Ncol];
+    hv[P.rFx + it] = !qp_rows_on(P, t, k) ? 0.0 : c < P.Ncol ? h0[k * P.Ncol + c] : P.desc.bx[c - P.Ncol];
     hv[P.rPos + it] = 0.0;
   }
   for (int it = ex.lane; it < P.U * P.nFu; it += ex.nlanes) hv[P.rFu + it] = P.desc.bu[it % P.nFu];
@@ -155,7 +155,7 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const gdouble* ws = C.ws;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const gdouble* H = ws + L.hx + k * NX * NX;
@@ -168,7 +168,7 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   for (int u = ex.lane; u < P.U; u += ex.nlanes) {
     const gdouble* Hu = ws + L.hu + u * NU * NU;
     const gdouble* O = ws + L.qo + u * NU * NU;
-    const int pu = qp_pred_u(P, u);
+    const int pu = qp_pred_u(t, u);
     double v[NU];
     for (int r = 0; r < NU; ++r) {
       double a = 0.0;
@@ -199,13 +199,13 @@ BMPC_FN void qp_apply_G(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.ws + L.dh;
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     double v = -zv[P.oS + it];
-    if (qp_rows_on(P, k))
+    if (qp_rows_on(P, t, k))
       for (int j = 0; j < NX; ++j) v += qp_row<NX>(P, dh, k, c, j) * zv[P.oX + k * NX + j];
     return v;
   }, [&](int it, double v) { out[P.rFx + it] = v; });
@@ -225,7 +225,7 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.ws + L.dh;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -234,7 +234,7 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble*
     const bool term = t.x_u[k] < 0;
     for (int c = 0; c < Nc; ++c) {
       const double rv = r[P.rFx + k * Nc + c];
-      if (qp_rows_on(P, k))
+      if (qp_rows_on(P, t, k))
         for (int j = 0; j < NX; ++j) ax[j] += qp_row<NX>(P, dh, k, c, j) * rv;
       out[P.oS + k * Nc + c] = -rv - r[P.rPos + k * Nc + c];
     }
@@ -257,7 +257,7 @@ template <class X, int NX, int NU>
 BMPC_FN void qp_apply_E(const X ex, const QpCtx Cin, const gdouble* zv, gdouble* out) {
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const gdouble* Ad = C.ws + C.L->Ad;
   const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -278,7 +278,7 @@ template <class X, int NX, int NU>
 BMPC_FN void qp_apply_ET(const X ex, const QpCtx Cin, const gdouble* y, gdouble* out) {
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const gdouble* Ad = C.ws + C.L->Ad;
   const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -317,7 +317,7 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
   constexpr int NS = NX + NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const double qs2 = 2.0 * P.desc.Qslack[0];
@@ -342,7 +342,7 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
         // reduced x Hessian: Hx + sum_c omega_c f_c f_c'
         double Hx[NX][NX];
         mat_load(Hx, ws + L.hx + k * NX * NX);
-        if (qp_rows_on(P, k))
+        if (qp_rows_on(P, t, k))
           for (int c = 0; c < Nc; ++c) {
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double om = df - df * df / sd;
@@ -456,7 +456,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
   constexpr int NS = NX + NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  auto& t = P.t;
+  const TopoL t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const gdouble* dh = ws + L.dh;
@@ -475,7 +475,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
         const bool term = t.x_u[k] < 0;
         double qx[NX];
         for (int j = 0; j < NX; ++j) qx[j] = -r[P.oX + k * NX + j];
-        if (qp_rows_on(P, k))
+        if (qp_rows_on(P, t, k))
           for (int c = 0; c < Nc; ++c) {   // slack elimination
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double a = df * r[P.oS + k * Nc + c] / sd;
@@ -562,7 +562,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
         for (int c = 0; c < Nc; ++c) {   // slack recovery
           const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
           double fx = 0.0;
-          if (qp_rows_on(P, k))
+          if (qp_rows_on(P, t, k))
             for (int j = 0; j < NX; ++j) fx += qp_row<NX>(P, dh, k, c, j) * s[j];
           out[P.oS + k * Nc + c] = (r[P.oS + k * Nc + c] + df * fx) / sd;
         }

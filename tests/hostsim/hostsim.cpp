@@ -22,6 +22,7 @@ struct HostExec {
   int lane = 0;
   int nlanes = 1;
   double* lds = nullptr;      // stands in for the wave's LDS scratch
+  const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
   static constexpr int kTaskLanes = 1;
   double tsum(double v) const { return v; }
   template <int S>
@@ -101,6 +102,7 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   HostExec ex;
   std::vector<double> lds(P.nlds);
   ex.lds = lds.data();
+  ex.tab = P.t.br_depth;      // the host blob (first table at offset 0)
 #pragma omp for schedule(dynamic, 4)
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
