@@ -144,7 +144,7 @@ class BatchPlan:
     # ---- timing ---------------------------------------------------------------------------
     PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
               "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree", "G_lp", "G_cone", "napplyG",
-              "x1", "x2", "x3", "x4")
+              "ts_pre", "ts_bw", "ts_fw", "ts_post", "riccati")
 
     def counters(self):
         """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build)."""

@@ -945,6 +945,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
     }
   }
   ex.sync();
+  BMPC_TIC(t_ric);
   // ---- tree Riccati factorisation (leaves -> root), one lane per branch --------------------
   // The cost-to-go P runs backward along each branch in registers; only at a branch end are
   // the children's first-node P read back (written by the previous depth phase).
@@ -986,6 +987,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
     }
     ex.sync();
   }
+  BMPC_TOC(C.ws, L, 23, t_ric);
   return ex.max(bad) == 0.0;
 }
 
@@ -1073,6 +1075,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   const gdouble* sdv = ws + L.sd;
   const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
 
+  BMPC_TIC(t_pre);
   // ---- (1) pre-pass: qx0 = -r_x - sum_c f_c df r_S / sd (non-terminal nodes) -------------
   // two flat passes (the slack terms a_kc into LDS scratch, then the node sums): a loop
   // over c with loads inside would cost one round trip per c
@@ -1110,6 +1113,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   }
   ex.sync();
 
+  BMPC_TOC(C.ws, L, PROF_X1, t_pre);
+  BMPC_TIC(t_bw);
   // ---- (2a) backward sweep (leaves -> root) ----------------------------------------------
   // The per-node loads do not depend on the recursion: one memory round trip per node.
   for (int dep = P.NB; dep >= 0; --dep) {
@@ -1200,6 +1205,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     }
     ex.sync();
   }
+  BMPC_TOC(C.ws, L, PROF_X2, t_bw);
+  BMPC_TIC(t_fw);
   // ---- (2b) forward sweep (root -> leaves): x and u only ------------------------------------
   for (int it = ex.lane; it < nr * NX; it += ex.nlanes) {
     const int ri = it / NX, j = it % NX;
@@ -1287,6 +1294,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     ex.sync();
   }
 
+  BMPC_TOC(C.ws, L, PROF_X3, t_fw);
+  BMPC_TIC(t_post);
   // ---- (3) post-pass: nu_k = -(l_k + P_k x_k), slack recovery --------------------------------
   for (int ri = 0; ri < nr; ++ri) {
     gdouble* o = o0 + ri * os;
@@ -1312,6 +1321,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     }, [&](int it, double v) { o[P.oS + it] = v; });
   }
   ex.sync();
+  BMPC_TOC(C.ws, L, PROF_X4, t_post);
 }
 
 // dense LU with partial pivoting of the coupling system (row-major n x n, in LDS)
