@@ -14,7 +14,7 @@ import random
 
 import numpy as np
 
-from highway_branch_dyn import backup_brake, backup_lc, backup_maintain, lane_bdry_h, veh_col
+from highway_branch_dyn import backup_brake, backup_lc, backup_maintain, interpolant, lane_bdry_h, veh_col
 
 v0 = 20
 f0 = np.array([v0, 0, 0, 0])
@@ -161,6 +161,71 @@ def merge_geometry(N_lane, merge_lane, merge_s, merge_R, merge_side=0):
     return X1, X2, Y1, Y2, psi1, psi2
 
 
+class Highway_env_merge:
+    """Merge scene (Highway_env_branch.py:271-390): the ego starts on the ramp (laneID 1),
+    the obstacle on the main road.
+
+    Per step: a vehicle past merge_s + 8 switches to laneID 0; every vehicle's backup
+    rollouts come from pred_model[laneID] (:326-331); the obstacle keeps backup policy 0 --
+    the reference computes an argmax over its policies and then overwrites every backupidx
+    with 0 (:334-345), so only the overwrite is kept here; the ego solves with the S, x_ref and
+    bx of its lane: identity / the last lane centre / the plan's bound on the main road, the
+    ramp's tangent transformation and bounds from the lane-reference interpolants on the
+    ramp (:350-364)."""
+
+    def __init__(self, NV, N_lane, mpc, pred_model, merge_lane=2, merge_s=50, merge_R=300, merge_side=0, dt=0.05):
+        self.dt, self.NV, self.N_lane = dt, NV, N_lane
+        self.laneID = [1] + [0] * (NV - 1)
+        self.merge_lane, self.merge_s, self.merge_R, self.merge_side = merge_lane, merge_s, merge_R, merge_side
+        self.pred_model, self.mpc = pred_model, mpc
+        self.backupcons = [pm.backupcons for pm in pred_model]
+        self.m = [len(b) for b in self.backupcons]
+        self.cons = mpc.predictiveModel.cons
+        self.LB = [self.cons.W / 2, N_lane * 3.6 - self.cons.W / 2]
+        X1, X2, Y1, Y2, psi1, psi2 = merge_geometry(N_lane, merge_lane, merge_s, merge_R, merge_side)
+        self.merge_theta = np.arccos(1 - lane_width * merge_lane / merge_R)
+        self.merge_end = merge_s + merge_R * np.sin(self.merge_theta)
+        self.merge_lane_ref_X = np.append(X1, X2)
+        self.merge_lane_ref_Y = np.append(Y1, Y2)
+        self.merge_lane_ref_psi = np.append(psi1, psi2)
+        self.refY = interpolant("refY", "linear", [self.merge_lane_ref_X], self.merge_lane_ref_Y)
+        self.refpsi = interpolant("refY", "linear", [self.merge_lane_ref_X], self.merge_lane_ref_psi)
+        x0 = np.array([[24, 13, v0, -0.2], [15, 5.4, v0, 0]], float)
+        self.veh_set = [vehicle(x0[i], dt=self.dt, backupidx=0) for i in range(NV)]
+        self.desired_x = [np.array([0, x0[i, 1], v0, 0], float) for i in range(NV)]
+
+    def transform(self, x):
+        """(S, x_ref, bx) of the ego's lane (:350-364)."""
+        if self.laneID[0] == 0:
+            return np.eye(4), np.array([0, (self.N_lane - 0.5) * 3.6, v0, 0], float), self.mpc.param.bx
+        y0, psi0 = float(self.refY(x[0])), float(self.refpsi(x[0]))
+        t = np.tan(psi0)
+        S = np.array([[1., 0, 0, 0], [-t, 1., 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]])
+        xRef = np.array([0, -t * x[0] + y0 + 1.8, v0, psi0])
+        bx = np.array([-t * x[0] + y0 + 3.6 * self.merge_lane - self.cons.W / 2, t * x[0] - y0 - self.cons.W / 2,
+                       psi0 + self.mpc.psimax, -psi0 + self.mpc.psimax])
+        return S, xRef, bx
+
+    def step(self, t_):
+        xx_set, u0_set = [None] * self.NV, [None] * self.NV
+        for i, veh in enumerate(self.veh_set):
+            if veh.state[0] > self.merge_s + 8:
+                self.laneID[i] = 0
+            xx_set[i] = self.pred_model[self.laneID[i]].zpred_eval(veh.state)
+        for i, veh in enumerate(self.veh_set):
+            veh.backupidx = 0
+            u0_set[i] = self.backupcons[self.laneID[i]][0](veh.state)
+        x = self.veh_set[0].state
+        S, xRef, bx = self.transform(x)
+        self.mpc.solve(self.veh_set[0].state, self.veh_set[1].state, xRef, S, Fx=None, bx=bx)
+        u_set = [self.mpc.uPred[0]] + u0_set[1:]
+        xPred, zPred, uPred, branch_w = self.mpc.BT2array()
+        for i, veh in enumerate(self.veh_set):
+            veh.step(u_set[i])
+        x_set = [v.state for v in self.veh_set]
+        return u_set, x_set, xx_set, xPred, zPred, branch_w
+
+
 def plot_snapshot(*args, **kwargs):
     """Plotting is out of scope for the MI355X build (matplotlib snapshot, :447)."""
     return None
@@ -181,5 +246,10 @@ def sim_overtake(mpc, N_lane):
     return rec
 
 
-def sim_merge(*args, **kwargs):
-    raise NotImplementedError("the merge scene (PredictiveModel_merge) is not built yet")
+def sim_merge(mpc, pred_model, N_lane, merge_lane, merge_s, merge_R, merge_side, T=6):
+    """The main_branch.py merge scene (:727-733): 2 vehicles, 6 s; returns the records."""
+    env = Highway_env_merge(2, N_lane, mpc, pred_model, merge_lane, merge_s, merge_R, merge_side, pred_model[0].dt)
+    rec = Highway_sim(env, T)
+    state_rec, input_rec, backup_rec, backup_choice_rec, xPred_rec, zPred_rec, branch_w_rec, collision = rec
+    animate_scenario(env, state_rec, backup_rec, backup_choice_rec, xPred_rec, zPred_rec, lm)
+    return rec

@@ -151,15 +151,33 @@ class BranchMPC_CVaR:
         return self._plan
 
     # ---- solve -----------------------------------------------------------------------------
+    def _transform(self, pl, S, bx, B):
+        """The S / bx arguments of solve (MPC_branch.py:2052-2057): S is reset on every call,
+        bx kept when None.  Only the merge model's plans take them (bmpc_set_transform)."""
+        merge = getattr(self.predictiveModel, "model_kind", None) == abi.MODEL_HIGHWAY_MERGE
+        if not merge:
+            if S is not None or bx is not None:
+                raise NotImplementedError("a state transformation S / per-step bx needs the merge model "
+                                          "(highway_branch_dyn.PredictiveModel_merge)")
+            return
+        S_arr = None if S is None else np.broadcast_to(np.asarray(S, float), (B, self.n, self.n))
+        bx_arr = None if bx is None else np.broadcast_to(_flat_bx(bx), (B, _flat_bx(bx).size))
+        pl.set_transform(S_arr, bx_arr)
+
     def solve(self, x, z, xRef=None, S=None, Fx=None, bx=None):
-        """One controller step (MPC_branch.py:2043-2092)."""
-        if S is not None or Fx is not None or bx is not None:
-            raise NotImplementedError("state transformation S / per-step Fx, bx (merge scene) not built yet")
+        """One controller step (MPC_branch.py:2043-2092); S / bx: the merge scene's state
+        transformation and state bound (PredictiveModel_merge controllers)."""
+        if Fx is not None:
+            raise NotImplementedError("a per-step Fx (no reference scene passes one)")
         if self.batch != 1:
             raise ValueError("this controller holds a batch; use solve_batch")
         if xRef is not None:
             self.xRef = xRef
+        self.S = S
+        if bx is not None:
+            self.bx = bx
         pl = self._ensure_plan()
+        self._transform(pl, S, bx, 1)
         t0 = datetime.datetime.now()
         r = pl.solve(np.asarray(x, float)[None], np.asarray(z, float)[None],
                      np.asarray(self.xRef, float)[None])
@@ -181,10 +199,12 @@ class BranchMPC_CVaR:
         self._bt = None            # rebuilt from the device tree on first access of .BT
         self._tree = None
 
-    def solve_batch(self, X, Z, XREF):
+    def solve_batch(self, X, Z, XREF, S=None, bx=None):
         """Batched step for all egos of the plan: returns the raw result dict
-        (upred [B,U,d], xpred [B,T,n], branch_w, J, status, iters)."""
+        (upred [B,U,d], xpred [B,T,n], branch_w, J, status, iters); S [B,n,n] / bx [B,nFx]
+        as in solve (merge model)."""
         pl = self._ensure_plan()
+        self._transform(pl, S, bx, self.batch)
         t0 = datetime.datetime.now()
         r = pl.solve(X, Z, XREF)
         self.solverTime = datetime.datetime.now() - t0

@@ -77,6 +77,7 @@ _SIGS = {
     "bmpc_set_warm_start": (C.c_int, [C.c_void_p] * 5),
     "bmpc_get_robust_warm_start": (C.c_int, [C.c_void_p] * 4),
     "bmpc_set_robust_warm_start": (C.c_int, [C.c_void_p] * 5),
+    "bmpc_set_transform": (C.c_int, [C.c_void_p] * 5),
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),

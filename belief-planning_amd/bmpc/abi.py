@@ -8,7 +8,7 @@ import numpy as np
 MAX_N, MAX_D, MAX_FX, MAX_FU, MAX_M = 8, 4, 8, 8, 4
 
 CTRL_CVAR, CTRL_PROX, CTRL_QP, CTRL_ROBUST = 0, 1, 2, 3
-MODEL_HIGHWAY, MODEL_QUADRUPED = 0, 1
+MODEL_HIGHWAY, MODEL_QUADRUPED, MODEL_HIGHWAY_MERGE = 0, 1, 2
 POL_MAINTAIN, POL_BRAKE, POL_LC, POL_MAINTAIN_TRACKV, POL_FORWARD, POL_STOP = range(6)
 
 (INFO_T, INFO_U, INFO_BDIM, INFO_NBRANCH, INFO_NV, INFO_NEQ, INFO_NROWS, INFO_NCONES,

@@ -115,6 +115,17 @@ class BatchPlan:
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         check(lib().bmpc_set_warm_start(self._h, _p(uLin), _p(p), _p(jc), _p(old), _p(m)), "bmpc_set_warm_start")
 
+    def set_transform(self, S=None, bx=None, s_on=None, mask=None):
+        """Per-ego state transformation S [B,n,n] (None = "S is None" for every ego) and
+        state bound bx [B,nFx] (None = keep) of the next solves -- the S / bx arguments of
+        BranchMPC_CVaR.solve (MPC_branch.py:2043-2057); HIGHWAY_MERGE plans only."""
+        B, n = self.batch, self.desc.n
+        S = None if S is None else np.ascontiguousarray(np.asarray(S, np.float64).reshape(B, n, n))
+        bx = None if bx is None else np.ascontiguousarray(np.asarray(bx, np.float64).reshape(B, self.desc.nFx))
+        on = None if s_on is None else np.ascontiguousarray(s_on, np.uint8)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_set_transform(self._h, _p(S), _p(on), _p(bx), _p(m)), "bmpc_set_transform")
+
     def get_robust_warm_start(self):
         """robustMPC's warm start: xLin [B,T,n], uLin [B,U,d], OldInput [B,d]."""
         B, n, d = self.batch, self.desc.n, self.desc.d

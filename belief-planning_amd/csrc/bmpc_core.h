@@ -95,6 +95,16 @@ typedef const BMPC_AS_LDS int32_t lint;
 typedef TopoT<gint*> Topo;
 typedef TopoT<lint*> TopoL;
 
+// transform slots (Layout::xform): S row-major, bx, "S is not None", "bx was set"
+enum { XF_S = 0, XF_BX = BMPC_MAX_N * BMPC_MAX_N, XF_SON = XF_BX + BMPC_MAX_FX, XF_BXSET = XF_SON + 1,
+       XF_COUNT = XF_BXSET + 1 };
+
+// Per-ego constants of a transform-capable solve (X::kTransform), formed once per solve in
+// the wave's LDS: Fx S, W1 S, (W1 S)'(W1 S) and bx (MPC_branch.py:1894-1901,1935-1937);
+// without S (or for the other models) the plan's Fx, W1, QQ, bx are read directly.
+enum { ECO_FX = 0, ECO_W1 = BMPC_MAX_FX * BMPC_MAX_N, ECO_QQ = ECO_W1 + BMPC_MAX_N * BMPC_MAX_N,
+       ECO_BX = ECO_QQ + BMPC_MAX_N * BMPC_MAX_N, ECO_COUNT = ECO_BX + BMPC_MAX_FX };
+
 struct Plan {
   bmpc_plan_desc desc;
   int n, d, N, NB, m, nFx, nFu, Nc;
@@ -123,6 +133,27 @@ struct Plan {
   int toff[BMPC_TOPO_N];   // offset of each table in the blob (int32 units)
   int ntab;                // blob length (int32 units); its LDS copy follows the nlds doubles
 };
+
+template <class X>
+BMPC_HD double fxv(const BMPC_AS_CONST Plan& P, const X& ex, int r, int j) {
+  if constexpr (X::kTransform) return ex.eco[ECO_FX + r * P.n + j];
+  else return P.desc.Fx[r * P.n + j];
+}
+template <class X>
+BMPC_HD double w1v(const BMPC_AS_CONST Plan& P, const X& ex, int r, int j) {
+  if constexpr (X::kTransform) return ex.eco[ECO_W1 + r * P.n + j];
+  else return P.W1[r * P.n + j];
+}
+template <class X>
+BMPC_HD double qqv(const BMPC_AS_CONST Plan& P, const X& ex, int i, int j) {
+  if constexpr (X::kTransform) return ex.eco[ECO_QQ + i * P.n + j];
+  else return P.QQ[i * P.n + j];
+}
+template <class X>
+BMPC_HD double bxv(const BMPC_AS_CONST Plan& P, const X& ex, int r) {
+  if constexpr (X::kTransform) return ex.eco[ECO_BX + r];
+  else return P.desc.bx[r];
+}
 
 // LDS view of the topology tables (ex.tab = the wave's copy of the blob)
 #define BMPC_TOPO_SET_(n) v.n = ex.tab + P.toff[i++];
@@ -156,6 +187,8 @@ struct Layout {
   size_t qo, qq, Pa, Ka, la;
   // robustMPC: carried linearisation trajectory, obstacle predictions [time][Ncol][n]
   size_t xlin, zrob;
+  // merge scene (HIGHWAY_MERGE plans): per-ego S [n*n], bx [BMPC_MAX_FX], flags (XF_*)
+  size_t xform;
   size_t stride;  // doubles per ego
 };
 
@@ -164,6 +197,8 @@ typedef const BMPC_AS_CONST Layout CLayout;
 
 // misc slots
 enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */, MISC_X0 = 8 /* n values (robustMPC) */ };
+
+
 
 // ------------------------------------------------------------------------------------
 // phase cycle counters: built with -DBMPC_PROFILE the device code accumulates s_memtime

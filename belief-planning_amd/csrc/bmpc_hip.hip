@@ -34,10 +34,13 @@ __device__ __forceinline__ double dpp_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
-struct DevExec {
+template <bool TR>
+struct DevExecT {
+  static constexpr bool kTransform = TR;   // per-ego S / bx constants in LDS (merge plans)
   int lane;
   ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm / k_qp only)
   lint* tab;     // this wave's LDS copy of the topology tables (k_ipm / k_qp only)
+  ldouble* eco;  // per-ego constants of the solve (ECO_*; kTransform only)
   static constexpr int nlanes = 64;
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
@@ -79,6 +82,8 @@ struct DevExec {
   }
 };
 
+using DevExec = DevExecT<false>;
+
 struct Bundle {
   Plan P;
   Layout L;
@@ -87,12 +92,22 @@ struct Bundle {
 // Dynamic LDS of the solver kernels: Plan::nlds doubles of scratch, then a copy of the
 // topology tables (Plan::ntab int32).  The copy is one batched pass at kernel start; every
 // later tree / cone / node-index lookup of the solve is an LDS read.
-__device__ __forceinline__ DevExec solver_exec(const Plan& P, double* lds_dyn) {
+// Dynamic LDS of the solver kernels: Plan::nlds doubles of scratch, then a copy of the
+// topology tables (Plan::ntab int32), then (transform-capable models) ECO_COUNT doubles of
+// per-ego constants.  The table copy is one batched pass at kernel start; every later tree /
+// cone / node-index lookup of the solve is an LDS read.
+__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform) {
+  const size_t tab = (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7;
+  return sizeof(double) * (size_t)P.nlds + tab + (transform ? sizeof(double) * ECO_COUNT : 0);
+}
+template <bool TR>
+__device__ __forceinline__ DevExecT<TR> solver_exec(const Plan& P, double* lds_dyn) {
   int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
   const int32_t* gtab = (const int32_t*)P.t.br_depth;   // blob base (the first table)
   for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];
   __syncthreads();
-  return DevExec{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl};
+  double* eco = lds_dyn + (solver_lds_bytes(P, false) / sizeof(double));
+  return DevExecT<TR>{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco};
 }
 
 template <class M>
@@ -104,7 +119,7 @@ __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, doubl
   if (e >= batch) return;
   const Plan& P = B->P;
   const Layout& L = B->L;
-  DevExec ex{(int)threadIdx.x, nullptr, nullptr};
+  DevExec ex{(int)threadIdx.x, nullptr, nullptr, nullptr};
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   BMPC_PROF(E.ws, L, PROF_TREE);
   tree_step<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
@@ -120,9 +135,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  const DevExec ex = solver_exec(P, lds_dyn);
+  const auto ex = solver_exec<M::kTransform>(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
-  IpmResult r = solve_ego_ipm<DevExec, M>(ex, P, L, E);
+  IpmResult r = solve_ego_ipm<DevExecT<M::kTransform>, M>(ex, P, L, E);
   const double* w = E.ws;
   const int lane = threadIdx.x;
   if (upred)
@@ -147,7 +162,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  const DevExec ex = solver_exec(P, lds_dyn);
+  const DevExec ex = solver_exec<false>(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
   IpmResult r = solve_ego_qp<DevExec, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -239,6 +254,28 @@ int fail(int code, const std::string& msg) {
     hipError_t _e = (expr);                                                                 \
     if (_e != hipSuccess) return fail(-5, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
+
+// device buffer owned by the scope (every early return of a HIPCHECK frees it)
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// host array -> fresh device copy (or null when the host pointer is null)
+hipError_t upload(DevBuf& b, const void* host, size_t bytes) {
+  if (!host) return hipSuccess;
+  hipError_t e = b.alloc(bytes);
+  if (e != hipSuccess) return e;
+  return hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice);
+}
 
 }  // namespace
 
@@ -401,19 +438,27 @@ int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask
 int bmpc_reset(bmpc_plan* pl, const uint8_t* mask) {
   if (!pl) return fail(-22, "null argument");
   HIPCHECK(hipSetDevice(pl->ctx->device));
-  uint8_t* d_mask = nullptr;
-  if (mask) {
-    HIPCHECK(hipMalloc(&d_mask, pl->batch));
-    HIPCHECK(hipMemcpy(d_mask, mask, pl->batch, hipMemcpyHostToDevice));
-  }
+  DevBuf d_mask;
+  HIPCHECK(upload(d_mask, mask, pl->batch));
   hipLaunchKernelGGL(k_reset, dim3((pl->batch + 255) / 256), dim3(256), 0, pl->stream, pl->d_ws,
-                     pl->hp.lay.stride, pl->hp.lay.misc, d_mask, pl->batch);
+                     pl->hp.lay.stride, pl->hp.lay.misc, d_mask.as<uint8_t>(), pl->batch);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(pl->stream));
-  if (d_mask) hipFree(d_mask);
   return 0;
 }
 
+// Scatter per-ego host rows [batch][cnt] into the slab at offset off (one staging copy;
+// masked egos only).  The stream is drained before the staging buffers go out of scope.
+static int scatter_rows(bmpc_plan* pl, const double* src, size_t off, int cnt, const uint8_t* d_mask) {
+  if (!src || cnt <= 0) return 0;
+  DevBuf buf;
+  HIPCHECK(upload(buf, src, sizeof(double) * (size_t)pl->batch * cnt));
+  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, pl->hp.lay.stride, off, cnt,
+                     buf.as<double>(), d_mask, pl->batch);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  return 0;
+}
 
 // Reads back the pending timing events (waits for the last instrumented solve).  The ring is
 // emptied on every exit path: a failed read-back drops the pending samples rather than leaving
@@ -439,7 +484,8 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
-  size_t lds_bytes = sizeof(double) * (size_t)P.nlds + ((sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7);
+  const bool merge = P.desc.model == BMPC_MODEL_HIGHWAY_MERGE;
+  size_t lds_bytes = solver_lds_bytes(P, merge);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
   if (const char* e = getenv("BMPC_IPM_LDS_BYTES")) {
@@ -453,6 +499,9 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_x, d_z, d_xref, B);
+  else if (merge)
+    hipLaunchKernelGGL(k_tree<HighwayMerge>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_x, d_z, d_xref, B);
   else
     hipLaunchKernelGGL(k_tree<Quadruped>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_x, d_z, d_xref, B);
@@ -461,6 +510,9 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
   if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(qp ? k_qp<Highway> : k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
+                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+  else if (merge)
+    hipLaunchKernelGGL(k_ipm<HighwayMerge>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
                        pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
   else
     hipLaunchKernelGGL(qp ? k_qp<Quadruped> : k_ipm<Quadruped>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
@@ -576,11 +628,8 @@ int bmpc_set_warm_start(bmpc_plan* pl, const double* uLin, const double* p, cons
   const Plan& P = pl->hp.plan;
   const Layout& L = pl->hp.lay;
   const int B = pl->batch;
-  uint8_t* dmask = nullptr;
-  if (mask) {
-    HIPCHECK(hipMalloc(&dmask, B));
-    HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
-  }
+  DevBuf dmask;
+  HIPCHECK(upload(dmask, mask, B));
   std::vector<double> ones(B, 1.0);
   struct Part { const double* src; size_t off; int cnt; };
   const Part parts[] = {{uLin, L.uLin, (P.U + 1) * P.d},
@@ -588,18 +637,8 @@ int bmpc_set_warm_start(bmpc_plan* pl, const double* uLin, const double* p, cons
                         {jcons, L.misc + MISC_JCONS, 1},
                         {old_input, L.misc + MISC_OLDU, P.d},
                         {ones.data(), L.misc + MISC_INIT, 1}};
-  for (const Part& pt : parts) {
-    if (!pt.src || pt.cnt <= 0) continue;
-    double* buf = nullptr;
-    HIPCHECK(hipMalloc(&buf, sizeof(double) * (size_t)B * pt.cnt));
-    HIPCHECK(hipMemcpy(buf, pt.src, sizeof(double) * (size_t)B * pt.cnt, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, pt.off, pt.cnt, buf,
-                       dmask, B);
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(pl->stream));
-    hipFree(buf);
-  }
-  if (dmask) hipFree(dmask);
+  for (const Part& pt : parts)
+    if (int rc = scatter_rows(pl, pt.src, pt.off, pt.cnt, dmask.as<uint8_t>())) return rc;
   return 0;
 }
 
@@ -624,29 +663,45 @@ int bmpc_set_robust_warm_start(bmpc_plan* pl, const double* xLin, const double* 
   const Plan& P = pl->hp.plan;
   const Layout& L = pl->hp.lay;
   const int B = pl->batch;
-  uint8_t* dmask = nullptr;
-  if (mask) {
-    HIPCHECK(hipMalloc(&dmask, B));
-    HIPCHECK(hipMemcpy(dmask, mask, B, hipMemcpyHostToDevice));
-  }
+  DevBuf dmask;
+  HIPCHECK(upload(dmask, mask, B));
   std::vector<double> ones(B, 1.0);
   struct Part { const double* src; size_t off; int cnt; };
   const Part parts[] = {{xLin, L.xlin, P.T * P.n},
                         {uLin, L.uLin, P.U * P.d},
                         {old_input, L.misc + MISC_OLDU, P.d},
                         {ones.data(), L.misc + MISC_INIT, 1}};
-  for (const Part& pt : parts) {
-    if (!pt.src || pt.cnt <= 0) continue;
-    double* buf = nullptr;
-    HIPCHECK(hipMalloc(&buf, sizeof(double) * (size_t)B * pt.cnt));
-    HIPCHECK(hipMemcpy(buf, pt.src, sizeof(double) * (size_t)B * pt.cnt, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, pl->stream, pl->d_ws, L.stride, pt.off, pt.cnt, buf,
-                       dmask, B);
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipStreamSynchronize(pl->stream));
-    hipFree(buf);
+  for (const Part& pt : parts)
+    if (int rc = scatter_rows(pl, pt.src, pt.off, pt.cnt, dmask.as<uint8_t>())) return rc;
+  return 0;
+}
+
+int bmpc_set_transform(bmpc_plan* pl, const double* S, const uint8_t* s_on, const double* bx, const uint8_t* mask) {
+  if (!pl) return fail(-22, "null argument");
+  const Plan& P = pl->hp.plan;
+  if (P.desc.model != BMPC_MODEL_HIGHWAY_MERGE)
+    return fail(-22, "bmpc_set_transform: only HIGHWAY_MERGE plans take a state transformation");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Layout& L = pl->hp.lay;
+  const int B = pl->batch, n = P.n, nF = P.nFx;
+  DevBuf dmask;
+  HIPCHECK(upload(dmask, mask, B));
+  // S (or zeros) and the "S is not None" flag of every masked ego
+  std::vector<double> Sv((size_t)B * n * n, 0.0), on(B, 0.0);
+  for (int e = 0; e < B; ++e) {
+    if (S) {
+      std::copy(S + (size_t)e * n * n, S + (size_t)(e + 1) * n * n, Sv.begin() + (size_t)e * n * n);
+      on[e] = (!s_on || s_on[e]) ? 1.0 : 0.0;
+    }
   }
-  if (dmask) hipFree(dmask);
+  // the slab keeps S at row stride n (XF_S holds n*n values)
+  if (int rc = scatter_rows(pl, Sv.data(), L.xform + XF_S, n * n, dmask.as<uint8_t>())) return rc;
+  if (int rc = scatter_rows(pl, on.data(), L.xform + XF_SON, 1, dmask.as<uint8_t>())) return rc;
+  if (bx) {
+    std::vector<double> ones(B, 1.0);
+    if (int rc = scatter_rows(pl, bx, L.xform + XF_BX, nF, dmask.as<uint8_t>())) return rc;
+    if (int rc = scatter_rows(pl, ones.data(), L.xform + XF_BXSET, 1, dmask.as<uint8_t>())) return rc;
+  }
   return 0;
 }
 
@@ -695,8 +750,10 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
                     double* dh) {
   if (!ctx || !desc || !policies || !x || !u || !z || B <= 0) return fail(-22, "null argument");
   const int n = desc->n, d = desc->d, m = desc->m, N = desc->N;
-  if ((desc->model == BMPC_MODEL_HIGHWAY && (n != 4 || d != 2)) ||
-      (desc->model == BMPC_MODEL_QUADRUPED && (n != 3 || d != 3)) || m < 1 || m > BMPC_MAX_M || N < 1)
+  if (((desc->model == BMPC_MODEL_HIGHWAY || desc->model == BMPC_MODEL_HIGHWAY_MERGE) && (n != 4 || d != 2)) ||
+      (desc->model == BMPC_MODEL_QUADRUPED && (n != 3 || d != 3)) ||
+      (desc->model != BMPC_MODEL_HIGHWAY && desc->model != BMPC_MODEL_HIGHWAY_MERGE &&
+       desc->model != BMPC_MODEL_QUADRUPED) || m < 1 || m > BMPC_MAX_M || N < 1)
     return fail(-22, "bad model dimensions");
   HIPCHECK(hipSetDevice(ctx->device));
   const size_t sizes[] = {(size_t)n * n, (size_t)n * d, (size_t)n, (size_t)n, (size_t)m,
@@ -704,10 +761,11 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
   double* hosts[] = {A, Bm, C, xp, p, dp, zpred, h0, dh};
   size_t tot = (size_t)B * (2 * n + d);
   for (size_t s : sizes) tot += (size_t)B * s;
-  double* buf = nullptr;
-  bmpc_policy* dpol = nullptr;
-  HIPCHECK(hipMalloc(&buf, tot * sizeof(double)));
-  HIPCHECK(hipMalloc(&dpol, sizeof(bmpc_policy) * (size_t)B * m));
+  DevBuf bbuf, bpol;
+  HIPCHECK(bbuf.alloc(tot * sizeof(double)));
+  HIPCHECK(bpol.alloc(sizeof(bmpc_policy) * (size_t)B * m));
+  double* buf = bbuf.as<double>();
+  bmpc_policy* dpol = bpol.as<bmpc_policy>();
   HIPCHECK(hipMemcpy(dpol, policies, sizeof(bmpc_policy) * (size_t)B * m, hipMemcpyHostToDevice));
   double* dxp = buf;
   double* dup = dxp + (size_t)B * n;
@@ -726,6 +784,9 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
   if (desc->model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_model<Highway>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
                        dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+  else if (desc->model == BMPC_MODEL_HIGHWAY_MERGE)
+    hipLaunchKernelGGL(k_model<HighwayMerge>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
   else
     hipLaunchKernelGGL(k_model<Quadruped>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
                        dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
@@ -733,8 +794,6 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
   HIPCHECK(hipDeviceSynchronize());
   for (int i = 0; i < 9; ++i)
     if (hosts[i] && dev[i]) HIPCHECK(hipMemcpy(hosts[i], dev[i], sizeof(double) * B * sizes[i], hipMemcpyDeviceToHost));
-  hipFree(buf);
-  hipFree(dpol);
   return 0;
 }
 
@@ -753,8 +812,9 @@ int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const do
   size_t tot = 0;
   for (size_t v : in_sz) tot += v;
   for (size_t v : out_sz) tot += (size_t)B * v;
-  double* buf = nullptr;
-  HIPCHECK(hipMalloc(&buf, tot * sizeof(double)));
+  DevBuf bbuf;
+  HIPCHECK(bbuf.alloc(tot * sizeof(double)));
+  double* buf = bbuf.as<double>();
   double* cur = buf;
   double* din[4];
   for (int i = 0; i < 4; ++i) {
@@ -773,7 +833,6 @@ int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const do
   HIPCHECK(hipDeviceSynchronize());
   for (int i = 0; i < 6; ++i)
     if (out_h[i]) HIPCHECK(hipMemcpy(out_h[i], dout[i], (size_t)B * out_sz[i] * sizeof(double), hipMemcpyDeviceToHost));
-  hipFree(buf);
   return 0;
 }
 

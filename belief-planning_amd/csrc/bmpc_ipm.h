@@ -163,10 +163,11 @@ BMPC_HD double cone_res(const X ex, const ConeGroups& G, const gdouble* v, int o
 // structured operators
 // ------------------------------------------------------------------------------------
 // x-coefficients of LP row c of state node k: c = 0 -> -dh_k, c >= 1 -> Fx[c-1]
-BMPC_HD double fx_coef(const Ctx& C, int k, int c, int j) {
+template <class X>
+BMPC_HD double fx_coef(const Ctx& C, const X& ex, int k, int c, int j) {
   CPlan& P = *C.P;
   if (c == 0) return -C.ws[C.L->dh + k * P.n + j];
-  return P.desc.Fx[(c - 1) * P.n + j];
+  return fxv(P, ex, c - 1, j);
 }
 
 // out(rows) = G zv, cone rows boosted
@@ -194,7 +195,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     double v = -S;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const double fd = dh[k * NX + j], fx = P.desc.Fx[cr * NX + j];
+      const double fd = dh[k * NX + j], fx = fxv(P, ex, cr, j);
       v += (on * (c == 0 ? -fd : fx)) * zv[P.oX + k * NX + j];
     }
     return Two{v, -S};
@@ -265,7 +266,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
         const int j = it / NX, r = it % NX;
         const int xk = ndx + j;
 #pragma unroll
-        for (int s2 = 0; s2 < NX; ++s2) v += -2.0 * P.W1[r * NX + s2] * zv[P.oX + xk * NX + s2];
+        for (int s2 = 0; s2 < NX; ++s2) v += -2.0 * w1v(P, ex, r, s2) * zv[P.oX + xk * NX + s2];
       } else {
         const int jj = it - nxn;
         const int j = jj / NU, r = jj % NU;
@@ -311,7 +312,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
       for (int s2 = 0; s2 < NX; ++s2) {
         double v = 0.0;
 #pragma unroll
-        for (int rr = 0; rr < NX; ++rr) v += -2.0 * P.W1[rr * NX + s2] * r[off + 1 + j * NX + rr];
+        for (int rr = 0; rr < NX; ++rr) v += -2.0 * w1v(P, ex, rr, s2) * r[off + 1 + j * NX + rr];
         cx[s2] = v - 2.0 * qx[s2] * f;
       }
       fS = Qs * f;
@@ -327,7 +328,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
       const double rv = r[P.rFx + k * Nc + c];
       if (!term)
 #pragma unroll
-        for (int j = 0; j < NX; ++j) ax[j] += (c == 0 ? -dhk[j] : P.desc.Fx[(c - 1) * NX + j]) * rv;
+        for (int j = 0; j < NX; ++j) ax[j] += (c == 0 ? -dhk[j] : fxv(P, ex, c - 1, j)) * rv;
       os[c] = -rv - r[P.rPos + k * Nc + c] + fS;
     }
     for (int c = 0; c < Nc; ++c) out[P.oS + k * Nc + c] = os[c] + sa * ad[P.oS + k * Nc + c];
@@ -496,7 +497,7 @@ BMPC_HD void build_hb(const X ex, const Ctx& C, gdouble* h, gdouble* bv) {
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
     const int k = it / Nc, c = it % Nc;
     double v = 0.0;
-    if (t.x_u[k] >= 0) v = c == 0 ? h0[k] : P.desc.bx[c - 1];
+    if (t.x_u[k] >= 0) v = c == 0 ? h0[k] : bxv(P, ex, c - 1);
     h[P.rFx + it] = v;
     h[P.rPos + it] = 0.0;
   }
@@ -868,7 +869,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
       if (!term) {
         const double om = df * dp / (df + dp);
         double f[NX];
-        for (int j = 0; j < NX; ++j) f[j] = fx_coef(C, k, c, j);
+        for (int j = 0; j < NX; ++j) f[j] = fx_coef(C, ex, k, c, j);
         for (int i = 0; i < NX; ++i)
           for (int j = 0; j < NX; ++j) H[i][j] += om * f[i] * f[j];
       }
@@ -877,7 +878,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
     if (kc >= 0) {
       const double sc = 4.0 / (eta[kc] * eta[kc]);
       for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) H[i][j] += sc * P.QQ[i * NX + j];
+        for (int j = 0; j < NX; ++j) H[i][j] += sc * qqv(P, ex, i, j);
     }
     mat_store(H, ws + L.hx + k * NX * NX);
   }
@@ -916,7 +917,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
         const gdouble* wu = wb + off + 1 + P.N * NX + it * NU;
         for (int s = 0; s < NX; ++s) {
           double v = 0.0;
-          for (int r = 0; r < NX; ++r) v += P.W1[r * NX + s] * wx[r];
+          for (int r = 0; r < NX; ++r) v += w1v(P, ex, r, s) * wx[r];
           g[P.oX + xk * NX + s] = kap * (-2.0 * qx[s]) + 2.0 * v;
         }
         for (int s = 0; s < NU; ++s) {
@@ -1094,7 +1095,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, j = it % NX;
         double v = -rr[P.oX + it] + dh[it] * av[k * Nc];
-        for (int c = 1; c < Nc; ++c) v -= P.desc.Fx[(c - 1) * NX + j] * av[k * Nc + c];
+        for (int c = 1; c < Nc; ++c) v -= fxv(P, ex, c - 1, j) * av[k * Nc + c];
         return v;
       }, [&](int it, double v) { q0[it] = v; });
       ex.sync();
@@ -1105,7 +1106,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         double v = -rr[P.oX + it];
         for (int c = 0; c < Nc; ++c) {
           const double a = sdv[(k * Nc + c) * 2 + 1] * rr[P.oS + k * Nc + c] / sdv[(k * Nc + c) * 2];
-          v -= on * (c == 0 ? -dh[it] : P.desc.Fx[(c - 1) * NX + j]) * a;
+          v -= on * (c == 0 ? -dh[it] : fxv(P, ex, c - 1, j)) * a;
         }
         return v;
       }, [&](int it, double v) { q0[it] = v; });
@@ -1316,7 +1317,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
       double fx = 0.0;
 #pragma unroll
-      for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : P.desc.Fx[(c - 1) * NX + j]) * o[P.oX + k * NX + j];
+      for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : fxv(P, ex, c - 1, j)) * o[P.oX + k * NX + j];
       return (rr[P.oS + it] + sdv[it * 2 + 1] * on * fx) / sdv[it * 2];
     }, [&](int it, double v) { o[P.oS + it] = v; });
   }

@@ -207,6 +207,7 @@ BMPC_HD S softmin2(const S& a, const S& b, double g) {
 // ------------------------------------------------------------------------------------
 struct Highway {
   static constexpr int NX = 4, NU = 2;
+  static constexpr bool kTransform = false;   // no per-ego S / bx (see HighwayMerge)
 
   template <class S, class T>
   BMPC_HD static void f(const S* x, const T* u, S* xd) {  // dubin (:17-34)
@@ -316,10 +317,48 @@ struct Highway {
 };
 
 // ------------------------------------------------------------------------------------
+// HighwayMerge: PredictiveModel_merge (highway_branch_dyn.py:400-502) as the merge scene's
+// controller uses it (pred_model[0], main_branch.py:85-88: maintain_trackV(v0) / brake, no
+// psiref): the highway dynamics, policies, collision row and branch probabilities, but
+// BF_traj (:463-467) is softmin_5 over veh_col(obs_k, ego_k, [L+1, W+0.2]) alone -- no
+// lane-boundary term.  Its plans carry a per-ego state transformation (kTransform).
+// ------------------------------------------------------------------------------------
+struct HighwayMerge : Highway {
+  static constexpr bool kTransform = true;
+
+  template <class S>
+  BMPC_HD static S bf_traj(const double* mc, double dt, int N, const bmpc_policy& ego_pol,
+                           const bmpc_policy& obs_pol, const S* x0, const double* z0) {
+    const double s0 = mc[0] + 1.0, s1 = mc[1] + 0.2;
+    S xe[4], ue[2], fe[4];
+    double zo[4], uo[2], fo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xe[i] = x0[i], zo[i] = z0[i];
+    S num = lift<S>(0.0), den = lift<S>(0.0);
+    for (int k = 0; k < N; ++k) {
+      policy(ego_pol, xe, ue);
+      f(xe, ue, fe);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xe[i] = xe[i] + fe[i] * dt;
+      policy(obs_pol, zo, uo);
+      f(zo, uo, fo);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) zo[i] = zo[i] + fo[i] * dt;
+      S h = veh_col(lift<S>(zo[0]), lift<S>(zo[1]), xe[0], xe[1], s0, s1);
+      S e = dexp(h * (-5.0));
+      num = num + e * h;
+      den = den + e;
+    }
+    return num / den;
+  }
+};
+
+// ------------------------------------------------------------------------------------
 // Quadruped: x = (X, Y, theta), u = (vx, vy, omega)   quadruped_branch_dyn.py:14-248
 // ------------------------------------------------------------------------------------
 struct Quadruped {
   static constexpr int NX = 3, NU = 3;
+  static constexpr bool kTransform = false;
 
   template <class S, class T>
   BMPC_HD static void f(const S* x, const T* u, S* xd) {  // quad_kinetics (:14-27)

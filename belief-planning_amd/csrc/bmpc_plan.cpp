@@ -101,8 +101,10 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
       desc.controller != BMPC_CTRL_ROBUST)
     return "unknown controller";
   const bool robust = desc.controller == BMPC_CTRL_ROBUST;
-  if (desc.model == BMPC_MODEL_HIGHWAY) {
+  if (desc.model == BMPC_MODEL_HIGHWAY || desc.model == BMPC_MODEL_HIGHWAY_MERGE) {
     if (n != 4 || d != 2) return "highway model needs n=4, d=2";
+    if (desc.model == BMPC_MODEL_HIGHWAY_MERGE && desc.controller != BMPC_CTRL_CVAR)
+      return "the merge model (state transformation S) is supported with the CVaR controller";
   } else if (desc.model == BMPC_MODEL_QUADRUPED) {
     if (n != 3 || d != 3) return "quadruped model needs n=3, d=3";
   } else {
@@ -428,6 +430,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   } else {
     L.qo = L.qq = L.Pa = L.Ka = L.la = 0;
   }
+  L.xform = take(XF_COUNT);
   L.xlin = robust ? take((size_t)T * n) : 0;
   L.zrob = robust ? take((size_t)(T - 1) * P.Ncol * n) : 0;
   L.stride = o;

@@ -26,6 +26,52 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
     }
     ws[L.misc + MISC_JCONS] = j;
   }
+  if constexpr (X::kTransform) {
+    // per-ego constants of this solve (MPC_branch.py:1894-1901,1935-1937): Fx S, W1 S,
+    // (W1 S)'(W1 S) when S is not None, else the plan's Fx, W1, QQ; the current bx
+    const double* xf = ws + L.xform;
+    const bool son = xf[XF_SON] != 0.0, bxset = xf[XF_BXSET] != 0.0;
+    const double* S = xf + XF_S;
+    const int nF = P.nFx;
+    for (int i = ex.lane; i < nF * NX + 2 * NX * NX + nF; i += ex.nlanes) {
+      double v;
+      if (i < nF * NX) {
+        const int r = i / NX, j = i % NX;
+        v = P.desc.Fx[r * NX + j];
+        if (son) {
+          v = 0.0;
+          for (int k = 0; k < NX; ++k) v += P.desc.Fx[r * NX + k] * S[k * NX + j];
+        }
+        ex.eco[ECO_FX + i] = v;
+      } else if (i < nF * NX + NX * NX) {
+        const int q = i - nF * NX, r = q / NX, j = q % NX;
+        v = P.W1[r * NX + j];
+        if (son) {
+          v = 0.0;
+          for (int k = 0; k < NX; ++k) v += P.W1[r * NX + k] * S[k * NX + j];
+        }
+        ex.eco[ECO_W1 + q] = v;
+      } else if (i < nF * NX + 2 * NX * NX) {
+        const int q = i - nF * NX - NX * NX, a = q / NX, b = q % NX;
+        v = P.QQ[a * NX + b];
+        if (son) {
+          v = 0.0;
+          for (int r = 0; r < NX; ++r) {
+            double wa = 0.0, wb = 0.0;
+            for (int k = 0; k < NX; ++k) {
+              wa += P.W1[r * NX + k] * S[k * NX + a];
+              wb += P.W1[r * NX + k] * S[k * NX + b];
+            }
+            v += wa * wb;
+          }
+        }
+        ex.eco[ECO_QQ + q] = v;
+      } else {
+        const int r = i - nF * NX - 2 * NX * NX;
+        ex.eco[ECO_BX + r] = bxset ? xf[XF_BX + r] : P.desc.bx[r];
+      }
+    }
+  }
   Ctx C;
   C.P = (CPlan*)&P;
   C.L = (CLayout*)&L;

@@ -122,6 +122,14 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
       for (int j = 0; j < n; ++j) dh[k * n + j] = 0.0;
     } else {
       col_eval<M>(mc, xbar + k * n, zbar + k * n, h0 + k, dh + k * n);
+      if constexpr (M::kTransform) {
+        // updateIneqConstr with S (MPC_branch.py:2025-2036): dh[0] <- sign(dh0) max(0.1, |dh0|)
+        // on every solve after the first; h0 keeps the unclipped dh (col_eval's h - dh.x)
+        if (init && ws[L.xform + XF_SON] != 0.0) {
+          const double a = dh[k * n];
+          dh[k * n] = a > 0.0 ? fmax(0.1, a) : a < 0.0 ? -fmax(0.1, -a) : 0.0;
+        }
+      }
     }
   }
   // ---- per-cone Lorentz boost of the rotated-cone rows ("cone boost") ----

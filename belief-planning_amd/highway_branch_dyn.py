@@ -16,7 +16,7 @@ from bmpc.tracing import PolicySpec, Tracer, trace
 
 __all__ = ["np", "dubin", "softsat", "backup_maintain", "backup_maintain_trackV", "backup_brake",
            "backup_lc", "softmin", "softmax", "propagate_backup", "lane_bdry_h", "veh_col",
-           "PredictiveModel", "PredictiveModel_merge"]
+           "PredictiveModel", "PredictiveModel_merge", "interpolant"]
 
 
 def dubin(x, u):
@@ -40,9 +40,39 @@ def softmax(x, gamma=1):
     return np.sum(e * x) / np.sum(e)
 
 
+class PsirefPolicy(NotImplementedError):
+    """A backup policy that tracks a lane-reference interpolant (the merge ramp): not
+    lowered to a GPU descriptor (see PredictiveModel_merge)."""
+
+
 def _psiref_unsupported():
-    raise NotImplementedError("psiref-tracking policies belong to the merge scene "
-                              "(PredictiveModel_merge), not lowered to the GPU in this version")
+    raise PsirefPolicy("psiref-tracking policies (the merge ramp's lane reference) are not lowered "
+                       "to GPU policy descriptors")
+
+
+class LinearInterpolant:
+    """``casadi.interpolant(name, 'linear', [grid], values)`` for the merge scene's lane
+    reference (main_branch.py:76-77, Highway_env_branch.py:312-313): piecewise linear on the
+    grid cells, the end cells extended beyond the grid (CasADi's 'linear' plugin)."""
+
+    def __init__(self, name, grid, values):
+        self.name = name
+        self.g = np.asarray(grid, float).reshape(-1)
+        self.v = np.asarray(values, float).reshape(-1)
+
+    def __call__(self, t):
+        t = np.asarray(t, float)
+        i = np.clip(np.searchsorted(self.g, t, side="right") - 1, 0, self.g.size - 2)
+        g0, g1, v0, v1 = self.g[i], self.g[i + 1], self.v[i], self.v[i + 1]
+        r = v0 + (t - g0) / (g1 - g0) * (v1 - v0)
+        return float(r) if r.ndim == 0 else r
+
+
+def interpolant(name, solver, grid, values, *opts):
+    """CasADi ``interpolant`` subset used by the reference (1-D, 'linear')."""
+    if solver != "linear" or len(grid) != 1:
+        raise NotImplementedError("only 1-D linear interpolants (the merge lane reference)")
+    return LinearInterpolant(name, grid[0], values)
 
 
 def backup_maintain(x, cons, psiref=None):
@@ -185,9 +215,70 @@ class PredictiveModel:
         return (r["h0"][0], r["dh"][0]) if np.ndim(x) == 1 else (r["h0"], r["dh"])
 
 
-class PredictiveModel_merge:
-    """Merge-scene model (:400-502): CasADi MX + linear ``interpolant`` lane reference.
-    Not built in this version."""
+class PredictiveModel_merge(PredictiveModel):
+    """``highway_branch_dyn.PredictiveModel_merge`` (:400-502): the highway model whose
+    ``BF_traj`` is softmin_5 of veh_col(obstacle, ego, [L+1, W+0.2]) only (:463-467).
 
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError("PredictiveModel_merge (sim_merge scene) is not built yet")
+    With plain policies -- the merge scene's controller model, ``pred_model[0]`` of
+    ``main_branch.sim_merge`` (maintain_trackV(v0), brake) -- it runs on the GPU (model kind
+    HIGHWAY_MERGE; its plans take the per-solve S / bx of ``BranchMPC_CVaR.solve``).  With
+    policies that track the ramp's lane reference (``psiref``, ``pred_model[1]``) the scene
+    only asks it for the ego's own backup rollouts (``zpred_eval``, recorded by the env,
+    ``Highway_env_branch.py:331``); those rollouts are evaluated from the policies' NumPy
+    branches (same expressions as the MX branches the reference compiles: maintain_trackV
+    [0.5(v0 - v), psiref(X) - Kpsi psi], brake [softmax([-5, -v], 3), psiref(X) - Kpsi psi]),
+    and such a model cannot drive a controller."""
+
+    model_kind = abi.MODEL_HIGHWAY_MERGE
+
+    def __init__(self, n, d, N, backupcons, dt, cons, merge_ref, laneID=0, N_lane1=3, N_lane2=2):
+        if (n, d) != (4, 2):
+            raise ValueError("the highway model is 4-state / 2-input")
+        self.n, self.d, self.N, self.dt, self.cons = n, d, N, dt, cons
+        self.N_lane2, self.laneID = N_lane2, laneID
+        self.refY, self.refpsi = merge_ref[0], merge_ref[1]
+        self.LB1 = [cons.W / 2, N_lane1 * 3.6 - cons.W / 2]
+        self.N_lane, self.LB = N_lane1, self.LB1
+        self.update_backup(backupcons)
+
+    def update_backup(self, backupcons):
+        self.backupcons = backupcons
+        self.m = len(backupcons)
+        try:
+            self.policies = trace(backupcons)
+            self.host_rollouts = False
+        except PsirefPolicy:
+            self.policies = None
+            self.host_rollouts = True
+
+    def policy_rows(self):
+        if self.host_rollouts:
+            raise PsirefPolicy("a PredictiveModel_merge with psiref policies cannot drive a controller")
+        return super().policy_rows()
+
+    def _eval(self, x, u, z):
+        if self.host_rollouts:     # dynamics / collision rows do not depend on the policies
+            x = np.atleast_2d(np.asarray(x, float))
+            rows = [[(abi.POL_MAINTAIN, (float(self.cons.Kpsi),))] * self.m] * x.shape[0]
+            from bmpc import plan
+            B = x.shape[0]
+            u = np.zeros((B, self.d)) if u is None else np.broadcast_to(np.atleast_2d(u), (B, self.d))
+            z = x if z is None else np.broadcast_to(np.atleast_2d(np.asarray(z, float)), (B, self.n))
+            return plan.model_eval(self.desc(), rows, x, u, z)
+        return super()._eval(x, u, z)
+
+    def branch_eval(self, x, z):
+        if self.host_rollouts:
+            raise PsirefPolicy("branch probabilities of psiref policies are not built (the scene never asks)")
+        return super().branch_eval(x, z)
+
+    def zpred_eval(self, z):
+        if not self.host_rollouts:
+            return super().zpred_eval(z)
+        z = np.asarray(z, float)
+        one = z.ndim == 1
+        out = []
+        for zz in np.atleast_2d(z):
+            cols = [propagate_backup(zz, lambda v, f=f: dubin(v, f(v)), self.N, self.dt) for f in self.backupcons]
+            out.append(np.hstack(cols))
+        return out[0] if one else np.array(out)

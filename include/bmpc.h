@@ -62,8 +62,13 @@ enum {
 
 /* predictive models */
 enum {
-  BMPC_MODEL_HIGHWAY = 0,   /* highway_branch_dyn.PredictiveModel   */
-  BMPC_MODEL_QUADRUPED = 1  /* quadruped_branch_dyn.PredictiveModel */
+  BMPC_MODEL_HIGHWAY = 0,       /* highway_branch_dyn.PredictiveModel   */
+  BMPC_MODEL_QUADRUPED = 1,     /* quadruped_branch_dyn.PredictiveModel */
+  BMPC_MODEL_HIGHWAY_MERGE = 2  /* highway_branch_dyn.PredictiveModel_merge (:400-502) without
+                                   psiref policies: BF_traj = softmin_5 of veh_col(obs, ego,
+                                   [L+1, W+0.2]) only (:463-467); plans of this model accept a
+                                   per-ego state transformation S and state bound bx
+                                   (bmpc_set_transform) -- the merge scene's controller */
 };
 
 /* backup-policy kinds (what the traced lambdas lower to) */
@@ -179,6 +184,20 @@ int bmpc_set_robust_warm_start(bmpc_plan* plan, const double* xLin, const double
                                const double* old_input, const uint8_t* mask);
 int bmpc_set_warm_start(bmpc_plan* plan, const double* uLin, const double* p,
                         const double* jcons, const double* old_input, const uint8_t* mask);
+
+/* Per-ego state transformation S and state bound bx of the next solves: the S / bx arguments
+ * of BranchMPC_CVaR.solve(x, z, xRef, S, Fx=None, bx) (MPC_branch.py:2043-2057), used by the
+ * merge scene (Highway_env_branch.py:358-367).  HIGHWAY_MERGE plans only.
+ *   S    [batch][n][n] row-major, or NULL = S is None for every ego (the reference resets
+ *        self.S on every solve, so pass it before each solve);
+ *   s_on [batch] (NULL = 1 for all egos when S is given): 0 marks "S is None" for that ego;
+ *   bx   [batch][nFx], or NULL = keep the current bound (the reference keeps self.bx).
+ * With S on, the state rows are Fx S x <= bx, the cones' middle rows use W1 S
+ * (buildIneqConstr :1894-1901,:1935-1937) and, on updates, the collision row's dh[0] is
+ * pushed to sign(dh0) max(0.1, |dh0|) while its rhs keeps the unclipped h0 (:2025-2036).
+ * mask NULL = all egos. */
+int bmpc_set_transform(bmpc_plan* plan, const double* S, const uint8_t* s_on, const double* bx,
+                       const uint8_t* mask);
 
 /* Tree of the last solve (host copies; NULL skips):
  *   xbar,zbar [batch][T][n]  ubar [batch][U][d]  w [batch][nbranch]

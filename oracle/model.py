@@ -322,6 +322,18 @@ class HighwayModel(_ModelBase):
         return self.veh_col(x, z, [self.L + 1.0, self.W + 0.2], 1.0)
 
 
+class HighwayMergeModel(HighwayModel):
+    """``highway_branch_dyn.PredictiveModel_merge`` (highway_branch_dyn.py:400-502) as the merge
+    scene's controller uses it (``pred_model[0]``, main_branch.py:85-88: maintain_trackV(v0) /
+    brake, no psiref): same dynamics, policies, collision row and branch probabilities as
+    the highway model; ``BF_traj`` (:463-467) is softmin_5 over veh_col(obs, ego, [L+1, W+0.2])
+    only -- no lane-boundary term."""
+
+    def bf_traj(self, x2, x1):
+        size = [self.L + 1.0, self.W + 0.2]
+        return softmin([self.veh_col(x2[k], x1[k], size) for k in range(len(x2))], 5.0)
+
+
 class QuadrupedModel(_ModelBase):
     """``quadruped_branch_dyn.PredictiveModel`` (quadruped_branch_dyn.py:154-248)."""
 

@@ -234,6 +234,8 @@ class CVaRController:
         self.last_problem = None
         self.last_info = None
         self.Solution = None
+        self.S = None            # state transformation of the current solve (merge scene)
+        self._first = True
 
     # ---- sizes ---------------------------------------------------------------------
     @property
@@ -304,11 +306,17 @@ class CVaRController:
         r0 = 0
         # Fxtot with slack (-I) ; only nodes i < len(utraj) get rows (terminal rows empty)
         hx = np.zeros(t.T * Nc)
+        # with a state transformation S (MPC_branch.py:1894-1901, :2025-2036): Fx S rows, and on
+        # updates dh[0] <- sign(dh0) max(0.1, |dh0|) in the row while h keeps the unclipped dh
+        FxS = self.Fx if self.S is None else self.Fx @ self.S
         for b in range(t.nbranch):
             for j in range(t.length[b]):
                 h0, dh = self.model.col_eval(tr.xtraj[b][j], tr.ztraj[b][j])
+                if self.S is not None and not self._first:
+                    dh = dh.copy()
+                    dh[0] = np.sign(dh[0]) * max(0.1, abs(dh[0]))
                 k = t.xnode(b, j)
-                blk = np.vstack((-dh, self.Fx))
+                blk = np.vstack((-dh, FxS))
                 for r in range(Nc):
                     for c in range(n):
                         if blk[r, c] != 0.0:
@@ -342,6 +350,7 @@ class CVaRController:
         # SOC cones (:1940-1984)
         qdims = []
         xq = self.xRef @ self.Q
+        W1 = self.Wx if self.S is None else self.Wx @ self.S      # :1935-1937
         for b in range(bd):
             for i, c in enumerate(t.children[b]):
                 nx = nu = t.length[c]
@@ -367,9 +376,9 @@ class CVaRController:
                     k = t.xnode(c, j)
                     for r in range(n):
                         for cc in range(n):
-                            if self.Wx[r, cc] != 0.0:
+                            if W1[r, cc] != 0.0:
                                 rows.append(f1r + 1 + j * n + r); cols.append(L['X'] + k * n + cc)
-                                vals.append(-2.0 * self.Wx[r, cc])
+                                vals.append(-2.0 * W1[r, cc])
                 for j in range(nu):
                     u = t.unode(c, j)
                     for r in range(d):
@@ -404,12 +413,17 @@ class CVaRController:
         return G, np.concatenate(h), {'l': n_lp, 'q': qdims}
 
     # ---- solve (:2043-2092) ------------------------------------------------------------
-    def setup_problem(self, x, z, xRef=None):
+    def setup_problem(self, x, z, xRef=None, S=None, bx=None):
+        """``solve`` (:2043-2057): xRef kept when None, S reset every solve, bx kept when None."""
         x = np.asarray(x, float)
         z = np.asarray(z, float)
         if xRef is not None:
             self.xRef = np.asarray(xRef, float)
+        self.S = None if S is None else np.asarray(S, float)
+        if bx is not None:
+            self.bx = np.asarray(bx, float).reshape(-1)
         first = self.tree is None
+        self._first = first
         if first:
             self.tree = TreeState(self.topo, self.n, self.d)
             self.Jcons = float(self.xRef @ self.Q @ self.xRef)
@@ -440,8 +454,8 @@ class CVaRController:
         out.append(0.5 * math.log(max(1.0, ub @ self.R @ ub)))
         return out
 
-    def solve(self, x, z, xRef=None):
-        prob = self.setup_problem(x, z, xRef)
+    def solve(self, x, z, xRef=None, S=None, bx=None):
+        prob = self.setup_problem(x, z, xRef, S, bx)
         sol, info = self.solver(prob)
         self.last_info = info
         self.accept(sol, info['exitFlag'])

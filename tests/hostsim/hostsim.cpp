@@ -18,11 +18,14 @@
 using namespace bmpc;
 
 namespace {
-struct HostExec {
+template <bool TR>
+struct HostExecT {
+  static constexpr bool kTransform = TR;
   int lane = 0;
   int nlanes = 1;
   double* lds = nullptr;      // stands in for the wave's LDS scratch
   const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
+  double* eco = nullptr;      // ... and for the per-ego constants (kTransform)
   static constexpr int kTaskLanes = 1;
   double tsum(double v) const { return v; }
   template <int S>
@@ -35,6 +38,7 @@ struct HostExec {
   double max(double v) const { return v; }
   double min(double v) const { return v; }
 };
+using HostExec = HostExecT<false>;
 
 struct HS {
   HostPlan hp;
@@ -100,15 +104,19 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
 #pragma omp parallel
   {
   HostExec ex;
-  std::vector<double> lds(P.nlds);
-  ex.lds = lds.data();
-  ex.tab = P.t.br_depth;      // the host blob (first table at offset 0)
+  HostExecT<true> exm;
+  std::vector<double> lds(P.nlds), eco(ECO_COUNT);
+  ex.lds = exm.lds = lds.data();
+  ex.tab = exm.tab = P.t.br_depth;      // the host blob (first table at offset 0)
+  exm.eco = eco.data();
 #pragma omp for schedule(dynamic, 4)
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;
     if (P.desc.model == BMPC_MODEL_HIGHWAY)
       r = solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY_MERGE)
+      r = solve_ego<HostExecT<true>, HighwayMerge>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
     else
       r = solve_ego<HostExec, Quadruped>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
     const double* ws = E.ws;
@@ -149,6 +157,24 @@ int hs_set_robust_warm_start(void* p, const double* xlin, const double* ulin, co
     memcpy(ws + L.uLin, ulin + (size_t)e * P.U * P.d, sizeof(double) * P.U * P.d);
     memcpy(ws + L.misc + MISC_OLDU, oldu + (size_t)e * P.d, sizeof(double) * P.d);
     ws[L.misc + MISC_INIT] = 1.0;
+  }
+  return 0;
+}
+
+// bmpc_set_transform of the host build (same slab slots)
+int hs_set_transform(void* p, const double* S, const uint8_t* s_on, const double* bx) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  const int n = P.n;
+  for (int e = 0; e < h->batch; ++e) {
+    double* xf = h->ws.data() + L.stride * e + L.xform;
+    for (int i = 0; i < n * n; ++i) xf[XF_S + i] = S ? S[(size_t)e * n * n + i] : 0.0;
+    xf[XF_SON] = (S && (!s_on || s_on[e])) ? 1.0 : 0.0;
+    if (bx) {
+      for (int i = 0; i < P.nFx; ++i) xf[XF_BX + i] = bx[(size_t)e * P.nFx + i];
+      xf[XF_BXSET] = 1.0;
+    }
   }
   return 0;
 }
@@ -200,6 +226,10 @@ int hs_model_eval(const bmpc_plan_desc* D, const bmpc_policy* pol, int B, const 
       model_eval_point<Highway>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
                                 OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n), OFF(zpred, N * m * n),
                                 OFF(h0, 1), OFF(dh, n));
+    else if (D->model == BMPC_MODEL_HIGHWAY_MERGE)
+      model_eval_point<HighwayMerge>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                     OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n), OFF(zpred, N * m * n),
+                                     OFF(h0, 1), OFF(dh, n));
     else
       model_eval_point<Quadruped>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
                                   OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),

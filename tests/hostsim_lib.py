@@ -110,6 +110,13 @@ class HostSim:
         oldu = None if oldu is None else np.ascontiguousarray(np.asarray(oldu, float).reshape(B, self.desc.d))
         lib().hs_set_warm_start(self.h, _p(uLin), _p(pprev), _p(jcons), _p(oldu))
 
+    def set_transform(self, S=None, bx=None, s_on=None):
+        B, n = self.batch, self.desc.n
+        S = None if S is None else np.ascontiguousarray(np.asarray(S, float).reshape(B, n, n))
+        bx = None if bx is None else np.ascontiguousarray(np.asarray(bx, float).reshape(B, self.desc.nFx))
+        on = None if s_on is None else np.ascontiguousarray(s_on, np.uint8)
+        lib().hs_set_transform(self.h, _p(S), _p(on), _p(bx))
+
     def set_robust_warm_start(self, xlin, ulin, oldu):
         xlin, ulin, oldu = (np.ascontiguousarray(a, dtype=np.float64) for a in (xlin, ulin, oldu))
         lib().hs_set_robust_warm_start(self.h, _p(xlin), _p(ulin), _p(oldu))

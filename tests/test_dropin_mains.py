@@ -38,6 +38,9 @@ class _HostPlan:
     def tree(self):
         return self._hs.tree()
 
+    def set_transform(self, S=None, bx=None, s_on=None, mask=None):
+        self._hs.set_transform(S, bx, s_on)
+
 
 @pytest.fixture
 def host_device(monkeypatch):
@@ -107,3 +110,27 @@ def test_bt_is_live_after_solve(host_device):
     first = mpc.BT
     mpc.solve(np.array([2, 1.8, 20, 0.]), np.array([7, 5.4, 20, 0.]), xRef)
     assert mpc.BT is not first              # rebuilt for the new solve
+
+
+def test_reference_sim_merge_runs_unchanged(host_device, monkeypatch):
+    """main_branch.sim_merge (reference :53-88): PredictiveModel_merge with linear
+    interpolants, BranchMPC_CVaR(ralpha=0.1) taking S / bx every step, Highway_env_merge --
+    shortened to 1 s and compared with the reference's own recording of the scene."""
+    import Highway_env_branch
+    from common import golden
+    full_sim = Highway_env_branch.Highway_sim
+    recs = []
+
+    def short(env, T):
+        recs.append(full_sim(env, 1.0))
+        return recs[-1]
+    monkeypatch.setattr(Highway_env_branch, "Highway_sim", short)
+    ns = runpy.run_path(os.path.join(REF, "main_branch.py"), run_name="ref_main_branch")
+    ns["sim_merge"]()
+    assert _HostPlan.solves == 10
+    g = golden("merge_n40_nb1")
+    state_rec, input_rec = recs[0][0], recs[0][1]
+    # Highway_sim records the state after each step: row t = traj_x[t+1]
+    np.testing.assert_allclose(state_rec[0][:9], g["traj_x"][1:10], atol=1e-6)
+    np.testing.assert_allclose(input_rec[0][:10], g["traj_u"][:10], atol=1e-5)
+    np.testing.assert_allclose(state_rec[1][:9], g["traj_z"][1:10], atol=1e-9)

@@ -667,7 +667,10 @@ class _Interp:
             return type(t)(out)
         if isinstance(t, DM):
             return DM(np.vectorize(self.value)(t.v))
-        return DM(self.value(float(t)))
+        # a scalar in gives a float out here (CasADi gives a 1x1 DM): the reference's NumPy
+        # branch np.array([0.5*(v0 - v), psiref(X) - Kpsi*psi]) (highway_branch_dyn.py:96) is a
+        # ragged list under NumPy >= 1.24 with a DM in it; its value is the same
+        return float(self.value(float(t)))
 
 
 def interpolant(name, solver, grid, values, *opts):

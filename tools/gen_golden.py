@@ -413,6 +413,91 @@ def gen_quadruped(name, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+def gen_merge(name, steps, keep, out):
+    """main_branch.sim_merge (main_branch.py:53-88): the reference's own merge scene --
+    PredictiveModel_merge over the CasADi shim (MX graphs with linear interpolants), the
+    reference's Highway_env_merge (Highway_env_branch.py:271-390) stepping it, and its
+    BranchMPC_CVaR taking the per-step S / bx (the S path of buildIneqConstr /
+    updateIneqConstr) with the oracle ECOS-algorithm IPM behind the ecos stub."""
+    ref_models()
+    import Highway_env_branch as HE
+    import highway_branch_dyn as H
+    import Init_MPC
+    import MPC_branch
+    from utils import Branch_constants
+
+    N, n, d, dt, NB, N_lane = 40, 4, 2, 0.1, 1, 2
+    xRef = np.array([0.5, 1.8, 15, 0])
+    am, rm = 7.0, 0.3
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20, s_c=1,
+                            ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    merge_lane, merge_s, merge_R, merge_side = 1, 50, 300, 0
+    X1, X2, Y1, Y2, psi1, psi2 = HE.merge_geometry(N_lane, merge_lane, merge_s, merge_R, merge_side)
+    refX, refYv, refpsiv = np.append(X1, X2), np.append(Y1, Y2), np.append(psi1, psi2)
+    refY = H.interpolant('refY', 'linear', [refX], refYv)
+    refpsi = H.interpolant('refpsi', 'linear', [refX], refpsiv)
+    v0 = HE.v0
+    bc_merge = [lambda x: H.backup_maintain_trackV(x, cons, v0, refpsi), lambda x: H.backup_brake(x, cons, refpsi)]
+    bc_normal = [lambda x: H.backup_maintain_trackV(x, cons, v0), lambda x: H.backup_brake(x, cons)]
+    pred_model = [H.PredictiveModel_merge(n, d, N, bc_normal, dt, cons, (refY, refpsi), laneID=0, N_lane1=N_lane,
+                                          N_lane2=merge_lane),
+                  H.PredictiveModel_merge(n, d, N, bc_merge, dt, cons, (refY, refpsi), laneID=1, N_lane1=N_lane,
+                                          N_lane2=merge_lane)]
+    param = Init_MPC.initBranchMPC(n, d, N, NB, xRef, am, rm, N_lane, cons.W)
+    mpc = MPC_branch.BranchMPC_CVaR(param, pred_model[0], ralpha=0.1)
+    CURRENT["mpc"] = mpc
+    env = HE.Highway_env_merge(2, N_lane, mpc, pred_model, merge_lane, merge_s, merge_R, merge_side,
+                               pred_model[0].dt)
+    args = {}
+    orig = mpc.solve
+
+    def recording_solve(x, z, xRef=None, S=None, Fx=None, bx=None):
+        args.update(x=np.array(x, float), z=np.array(z, float), xRef=np.array(xRef, float),
+                    S=np.array(S, float), bx=np.asarray(bx[0] if isinstance(bx, tuple) else bx, float).reshape(-1))
+        return orig(x, z, xRef, S, Fx, bx)
+    mpc.solve = recording_solve
+    d_out = dict(N=N, NB=NB, m=2, n=n, d=d, dt=dt, am=am, rm=rm, N_lane=N_lane, ralpha=0.1, v0=float(v0),
+                 L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef, Q=param.Q, R=param.R, Fx=param.Fx,
+                 bx=np.asarray(param.bx, float).reshape(-1), Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1),
+                 Qslack=param.Qslack, refX=refX, refY=refYv, refpsi=refpsiv)
+    traj = {k: [] for k in ("x", "z", "xRef", "S", "bx", "u", "exit", "J", "iters", "laneID", "ws_uLin", "ws_p",
+                            "obs_u", "ego_backup")}
+    for t in range(steps):
+        traj["ws_uLin"].append(None if mpc.uLin is None else np.array(mpc.uLin, float).copy())
+        traj["ws_p"].append(None if mpc.BT is None else
+                            np.array([np.ravel(b.p) for b in mpc.ndx if b.depth < NB], float))
+        u_set, x_set, xx_set, xPred, zPred, branch_w = env.step(t)
+        prob, sol, info, kw = CURRENT["captured"]
+        for k in ("x", "z", "xRef", "S", "bx"):
+            traj[k].append(args[k])
+        traj["u"].append(np.array(u_set[0], float))
+        traj["obs_u"].append(np.array(u_set[1], float))
+        traj["ego_backup"].append(np.array(xx_set[0], float))
+        traj["exit"].append(info["exitFlag"])
+        traj["J"].append(sol[-1])
+        traj["iters"].append(info["iter"])
+        traj["laneID"].append(int(env.laneID[0]))
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.G, p + "G", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "c"], d_out[p + "h"], d_out[p + "b"] = prob.c, prob.h, prob.b
+            d_out[p + "dims_l"] = np.array(prob.dims["l"])
+            d_out[p + "dims_q"] = np.array(prob.dims["q"])
+            d_out[p + "cone_boost"] = np.array(prob.cone_boost)
+            d_out[p + "sol"] = sol
+            d_out[p + "uPred"], d_out[p + "xPred"] = mpc.uPred, mpc.xPred
+        print(f"[{name}] t={t:3d} lane={env.laneID[0]} exit={info['exitFlag']:3d} it={info['iter']:3d} "
+              f"J={sol[-1]:.6f} u0={mpc.uPred[0]}", flush=True)
+    for k in ("ws_uLin", "ws_p"):
+        shape = next(v.shape for v in traj[k] if v is not None)
+        traj[k] = [np.full(shape, np.nan) if v is None else v for v in traj[k]]
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -431,6 +516,7 @@ def main():
         "highway_robust_n20_nb1": lambda: gen_highway_robust("highway_robust_n20_nb1", 20, 1, 5 if a.quick else 30, {0, 1, 2, 15}, out),
         "highway_robust_n8_nb2": lambda: gen_highway_robust("highway_robust_n8_nb2", 8, 2, 5 if a.quick else 20, {0, 1, 10}, out),
         "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
+        "merge_n40_nb1": lambda: gen_merge("merge_n40_nb1", 4 if a.quick else 60, {0, 1, 2, 30, 45}, out),
     }
     for k, f in jobs.items():
         if a.only and k not in a.only.split(","):

@@ -98,6 +98,38 @@ def gen_highway(H, utils, rng):
     return out
 
 
+def gen_merge_model(H, utils, rng):
+    """PredictiveModel_merge (highway_branch_dyn.py:400-502) as sim_merge's controller builds it:
+    pred_model[0] with [maintain_trackV(v0), brake] and no psiref (main_branch.py:85-88)."""
+    cons = utils.Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=7.0, rm=0.3, J_c=20, s_c=1,
+                                  ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    out = {}
+    for ci, (N, v0, K) in enumerate([(40, 20.0, 12), (10, 18.0, 8)]):
+        grid = np.linspace(0.0, 100.0, 11)
+        ref = (H.interpolant('refY', 'linear', [grid], np.linspace(9.0, 5.4, 11)),
+               H.interpolant('refpsi', 'linear', [grid], np.full(11, -0.05)))
+        model = H.PredictiveModel_merge(4, 2, N, [lambda x, v=v0: H.backup_maintain_trackV(x, cons, v),
+                                                  lambda x: H.backup_brake(x, cons)], 0.1, cons, ref, laneID=0,
+                                        N_lane1=2, N_lane2=1)
+        x, z, u = seeded_highway_points(K, rng)
+        rec = {k: [] for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")}
+        for k in range(K):
+            A, B, C, xp = model.dyn_linearization(x[k], u[k])
+            p, dp = model.branch_eval(x[k], z[k])
+            zp = model.zpred_eval(z[k])
+            h0, dh = model.col_eval(x[k], z[k])
+            for key, v in zip(rec, (A, B, C, xp, p, dp, zp, h0, dh)):
+                rec[key].append(np.asarray(v, float))
+        pre = f"c{ci}_"
+        out[pre + "N"], out[pre + "v0"] = N, v0
+        out[pre + "x"], out[pre + "z"], out[pre + "u"] = x, z, u
+        for key, v in rec.items():
+            out[pre + key] = np.array(v)
+    out["ncases"] = 2
+    out["dt"], out["L"], out["W"], out["s1"], out["Kpsi"] = 0.1, 4.0, 2.5, 2.0, 0.1
+    return out
+
+
 def gen_quadruped(Q, utils, rng):
     out = {}
     # (N, dt, v0, L1, W1, L2, W2, col_tol, K): main_quadruped.py:15-30, then the smoke test
@@ -180,6 +212,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "model_highway.npz"), **gen_highway(H, utils, rng))
     np.savez_compressed(os.path.join(OUT, "model_quadruped.npz"), **gen_quadruped(Q, utils, rng))
     np.savez_compressed(os.path.join(OUT, "model_hmm.npz"), **gen_hmm(HM, utils, rng))
+    np.savez_compressed(os.path.join(OUT, "model_merge.npz"), **gen_merge_model(H, utils, np.random.default_rng(77)))
     print("wrote", [f for f in os.listdir(OUT) if f.startswith("model_")])
 
 
