@@ -8,6 +8,7 @@ from __future__ import annotations
 import numpy as np
 
 from MPC_branch import BranchMPCParams
+from PredictiveControllers import MPC  # noqa: F401  (Init_MPC.py:4 re-exports the belief MPC)
 from utils import MPCParams
 
 LANE_WIDTH = 3.6

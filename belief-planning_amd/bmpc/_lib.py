@@ -24,7 +24,7 @@ class BmpcUnavailable(RuntimeError):
 
 
 def sources():
-    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_plan.cpp")]
+    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_plan.cpp", "bmpc_qpplan.cpp")]
 
 
 def headers():
@@ -83,6 +83,8 @@ _SIGS = {
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),
     "bmpc_hmm_eval": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 9),
     "bmpc_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 10),
+    "bmpc_qp_solve": (C.c_int, [C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 5
+                      + [C.c_int, C.c_double] + [C.c_void_p] * 5),
 }
 
 EXPORTED = tuple(_SIGS)

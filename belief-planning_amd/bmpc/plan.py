@@ -200,3 +200,53 @@ def hmm_eval(M, m, consts, xb, u, xbackup, device: int = 0):
     check(lib().bmpc_hmm_eval(context(device), M, m, _p(hc), B, _p(xb), _p(u), _p(xbk),
                               *(_p(out[k]) for k in ("xbp", "A", "B", "C", "h0", "Jh"))), "bmpc_hmm_eval")
     return out
+
+
+def qp_arrays(P, q, A, l, u):
+    """CSC arrays of one QP -- or of a batch sharing one pattern -- in bmpc_qp_solve's layout.
+
+    ``P`` / ``A`` are scipy sparse or dense matrices (or equal-length sequences of them); only
+    the upper triangle of P is kept (OSQP's interface does the same, PredictiveControllers.py:
+    325).  A batch's pattern is the union of its members' patterns."""
+    import scipy.sparse as sp
+    many = isinstance(P, (list, tuple))
+    Ps = [sp.triu(sp.csc_matrix(p), format="csc") for p in (P if many else [P])]
+    As = [sp.csc_matrix(a) for a in (A if many else [A])]
+    B = len(Ps)
+    n = Ps[0].shape[1]
+    m = As[0].shape[0]
+
+    def pattern(ms):
+        pat = sp.csc_matrix(ms[0].shape)
+        for mat in ms:
+            pat = pat + sp.csc_matrix((np.ones(mat.nnz), mat.indices, mat.indptr), shape=mat.shape)
+        pat = sp.csc_matrix(pat)
+        pat.sort_indices()
+        rows = pat.indices.astype(np.int64)
+        cols = np.repeat(np.arange(pat.shape[1]), np.diff(pat.indptr))
+        vals = np.stack([np.asarray(sp.csr_matrix(mat)[rows, cols]).reshape(-1) for mat in ms]) if len(rows) else \
+            np.zeros((len(ms), 0))
+        return pat.indptr.astype(np.int32), pat.indices.astype(np.int32), vals
+
+    Pp, Pi, Px = pattern(Ps)
+    Ap, Ai, Ax = pattern(As) if m else (np.zeros(n + 1, np.int32), np.zeros(0, np.int32), np.zeros((B, 0)))
+    def f2(a, k):
+        a = np.asarray(a, np.float64)
+        return np.ascontiguousarray(np.broadcast_to(a.reshape(-1, k) if k else np.zeros((B, 0)), (B, k)))
+    return dict(n=n, m=m, Pp=Pp, Pi=Pi, Ap=Ap, Ai=Ai, Px=np.ascontiguousarray(Px), q=f2(q, n),
+                Ax=np.ascontiguousarray(Ax), l=f2(l, m), u=f2(u, m))
+
+
+def qp_solve(P, q, A, l, u, max_iter: int = 100, eps: float = 1e-10, device: int = 0):
+    """OSQP-form QP(s)  min 1/2 x'Px + q'x  s.t. l <= Ax <= u  on the GPU (bmpc_qp_solve:
+    interior point on the band-ordered KKT matrix, one wave per problem).  Returns
+    dict(x [B][n], y [B][m], status [B] (1 solved, -2 max_iter, -8 numerics), iters [B],
+    info = (KKT dimension, bandwidth, inequality rows, band entries))."""
+    a = qp_arrays(P, q, A, l, u)
+    B, n, m = a["q"].shape[0], a["n"], a["m"]
+    x, y = np.zeros((B, n)), np.zeros((B, max(m, 1)))
+    st, it, info = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(4, np.int32)
+    check(lib().bmpc_qp_solve(context(device), n, m, _p(a["Pp"]), _p(a["Pi"]), _p(a["Ap"]), _p(a["Ai"]), B,
+                              _p(a["Px"]), _p(a["q"]), _p(a["Ax"]), _p(a["l"]), _p(a["u"]), int(max_iter),
+                              float(eps), _p(x), _p(y), _p(st), _p(it), _p(info)), "bmpc_qp_solve")
+    return dict(x=x, y=y[:, :m], status=st, iters=it, info=info)

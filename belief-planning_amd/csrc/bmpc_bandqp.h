@@ -1,0 +1,356 @@
+// bmpc_bandqp.h -- batched convex QP in OSQP's problem form
+//
+//     minimise 1/2 x'Px + q'x   subject to   l <= Ax <= u
+//
+// the solver behind the belief LTV-MPC (PredictiveControllers.MPC.osqp_solve_qp,
+// PredictiveControllers.py:310-340, which builds a fresh OSQP object per solve).  OSQP's
+// ADMM is not restated: like the oracle (oracle/qp_ipm.py) the kernel returns the QP optimum
+// by a Mehrotra predictor-corrector interior-point method.
+//
+// Rows are split by the host (bmpc_bandqp.cpp) into equalities (l == u) and one-sided
+// inequality copies (a'x <= u, -a'x <= -l).  Each Newton step solves the quasidefinite KKT
+// system
+//
+//     [ P + rI    E'     G'         ] [dx]
+//     [ E        -rI                ] [dy]   (r: static regularisation, removed again by
+//     [ G               -S/Z - rI   ] [dz]    iterative refinement on the true matrix)
+//
+// whose LDL' factorisation exists in ANY symmetric ordering.  The host orders the KKT
+// matrix by reverse Cuthill-McKee; an MPC's stage structure then leaves a narrow band
+// (bandwidth bw), so the factorisation costs nk*bw^2/2 instead of nk^3/3.
+//
+// Execution: one 64-lane wave per problem.  The factorisation streams the band through a
+// (bw+1) x (bw+1) ring window in LDS -- each rank-1 update touches only rows k+1..k+bw, so
+// every band entry is read from HBM once and written once per factorisation; the solve
+// vector lives in LDS too.  Everything else is O(nk*bw) per iteration.  Vectors are kept in
+// "KKT space" (the permuted index of the x, y and z blocks) so every IPM vector operation
+// is one strided loop.
+//
+// Written once for the executor X (bmpc_core.h): libbmpc.so runs it with the device wave,
+// tests/hostsim with the 1-lane host executor.
+#pragma once
+
+#include "bmpc_core.h"
+
+namespace bmpc {
+
+enum { QPK_X = 0, QPK_EQ = 1, QPK_IN = 2 };
+
+// problem statuses (OSQP's status_val codes where one exists)
+enum { QP_SOLVED = 1, QP_MAX_ITER = -2, QP_NUMERICS = -8 };
+
+// The symbolic part shared by every problem of a batch (one sparsity pattern, one row
+// classification); pointers refer to device memory on the GPU, host memory in hostsim.
+struct BandQPDesc {
+  int32_t n, m;          // variables, rows of A
+  int32_t nk, bw, W;     // KKT dimension, bandwidth after ordering, W = bw + 1
+  int32_t n_in;          // inequality copies (mu normaliser)
+  int32_t nvals, ncvals; // values per problem: [Px; Ax] and [q; l; u]
+  int32_t nscat, ncscat; // entries of the two scatter lists
+  int32_t max_iter;
+  double eps;            // convergence tolerance (oracle/qp_ipm.py's tol)
+  const int32_t* kind;   // [nk] QPK_* of each KKT row
+  const int32_t* scat;   // [nscat][3]: src in [Px; Ax], band index dst, sign
+  const int32_t* cscat;  // [ncscat][3]: src in [q; l; u], KKT index dst, sign
+  const int32_t* xmap;   // [n] KKT index of x_j
+  const int32_t* ymap;   // [m][4]: KKT index and sign of the eq / upper copy, of the lower copy (-1 none)
+  size_t stride;         // workspace doubles per problem
+};
+
+// workspace of one problem (doubles)
+struct BandQPWs {
+  double *Kb, *Lb, *c, *w, *s, *r, *dw, *rhs, *t1, *t2, *fdg, *tdg, *ds;
+};
+
+BMPC_HD size_t bandqp_stride(int nk, int W) { return 2 * (size_t)nk * W + 11 * (size_t)nk; }
+// LDS: the factorisation window (W*W), its column of multipliers (W), the solve vector (nk)
+BMPC_HD size_t bandqp_lds_doubles(int nk, int W) { return (size_t)W * W + W + nk; }
+
+BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
+  BandQPWs v;
+  const size_t nk = d.nk, band = nk * d.W;
+  v.Kb = base;
+  v.Lb = base + band;
+  double* p = base + 2 * band;
+  double** vecs[] = {&v.c, &v.w, &v.s, &v.r, &v.dw, &v.rhs, &v.t1, &v.t2, &v.fdg, &v.tdg, &v.ds};
+  for (double** q : vecs) {
+    *q = p;
+    p += nk;
+  }
+  return v;
+}
+
+// out = K v, K the symmetric band matrix Kb with its diagonal replaced by dg
+template <class X>
+BMPC_HD void bqp_matvec(const X& ex, const BandQPDesc& d, const double* Kb, const double* dg, const double* v,
+                        double* out) {
+  const int nk = d.nk, W = d.W, bw = d.bw;
+  for (int i = ex.lane; i < nk; i += ex.nlanes) {
+    double a = dg[i] * v[i];
+    const double* row = Kb + (size_t)i * W;
+    const int k0 = i < bw ? i : bw;
+    for (int k = 1; k <= k0; ++k) a += row[k] * v[i - k];
+    const int k1 = nk - 1 - i < bw ? nk - 1 - i : bw;
+    for (int k = 1; k <= k1; ++k) a += Kb[(size_t)(i + k) * W + k] * v[i + k];
+    out[i] = a;
+  }
+  ex.sync();
+}
+
+// Band LDL' of Kb with diagonal fdg (the regularised one) into Lb: row i of Lb holds
+// L[i][i-k] for k = 1..bw and D[i] at k = 0.  Right-looking, rows k..k+bw of the active
+// submatrix resident in the LDS ring window.  A pivot of the wrong sign or below 1e-13 in
+// magnitude is replaced by +-2e-7 (ECOS's dynamic regularisation constants).
+template <class X>
+BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, double* Lb) {
+  const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
+  auto* win = ex.lds;
+  auto* lv = ex.lds + (size_t)W * W;
+  const int rows0 = nk < W ? nk : W;
+  for (int t = ex.lane; t < rows0 * W; t += nl) {
+    const int i = t / W, k = t - i * W;
+    win[t] = k == 0 ? fdg[i] : Kb[(size_t)i * W + k];   // row i sits in slot i (i < W)
+  }
+  ex.sync();
+  for (int k = 0; k < nk; ++k) {
+    const int slot = k % W;
+    double dk = win[slot * W];
+    const double sg = d.kind[k] == QPK_X ? 1.0 : -1.0;
+    if (!(sg * dk >= 1e-13)) dk = sg * 2e-7;
+    const int last = nk - 1 - k < bw ? nk - 1 - k : bw;   // rows k+1 .. k+last
+    for (int a = ex.lane; a < last; a += nl) {
+      const int i = k + 1 + a;
+      const int si = i % W;
+      const double l = win[si * W + a + 1] / dk;
+      win[si * W + a + 1] = l;
+      lv[a] = l;
+    }
+    ex.sync();
+    for (int a = ex.lane; a < last; a += nl) {
+      const int si = (k + 1 + a) % W;
+      const double la = lv[a] * dk;
+      for (int b = 0; b <= a; ++b) win[si * W + a - b] -= la * lv[b];
+    }
+    ex.sync();
+    // row k is final: retire it to Lb and stream row k + W into its slot
+    const int nxt = k + W;
+    for (int c = ex.lane; c < W; c += nl) {
+      Lb[(size_t)k * W + c] = c == 0 ? dk : win[slot * W + c];
+      if (nxt < nk) win[slot * W + c] = c == 0 ? fdg[nxt] : Kb[(size_t)nxt * W + c];
+    }
+    ex.sync();
+  }
+}
+
+// out = (L D L')^{-1} b; column sweeps on the LDS solve vector
+template <class X>
+BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const double* Lb, const double* b, double* out) {
+  const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
+  auto* y = ex.lds + (size_t)W * W + W;
+  for (int i = ex.lane; i < nk; i += nl) y[i] = b[i];
+  ex.sync();
+  for (int k = 0; k < nk; ++k) {            // L y = b
+    const double yk = y[k];
+    const int last = nk - 1 - k < bw ? nk - 1 - k : bw;
+    for (int a = 1 + ex.lane; a <= last; a += nl) y[k + a] -= Lb[(size_t)(k + a) * W + a] * yk;
+    ex.sync();
+  }
+  for (int i = ex.lane; i < nk; i += nl) y[i] /= Lb[(size_t)i * W];
+  ex.sync();
+  for (int k = nk - 1; k > 0; --k) {        // L' x = y
+    const double xk = y[k];
+    const int last = k < bw ? k : bw;
+    for (int a = 1 + ex.lane; a <= last; a += nl) y[k - a] -= Lb[(size_t)k * W + a] * xk;
+    ex.sync();
+  }
+  for (int i = ex.lane; i < nk; i += nl) out[i] = y[i];
+  ex.sync();
+}
+
+// out = K^{-1} b for the true matrix (Kb, diagonal tdg) through its regularised factor:
+// up to three refinement steps, stopping at a 1e-15 relative residual (oracle/qp_ipm.py).
+template <class X>
+BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs& v, const double* b, double* out) {
+  bqp_ldl_solve(ex, d, v.Lb, b, out);
+  double bn = 0.0;
+  for (int i = ex.lane; i < d.nk; i += ex.nlanes) bn = fmax(bn, fabs(b[i]));
+  bn = ex.max(bn);
+  for (int it = 0; it < 3; ++it) {
+    bqp_matvec(ex, d, v.Kb, v.tdg, out, v.t1);
+    double rn = 0.0;
+    for (int i = ex.lane; i < d.nk; i += ex.nlanes) {
+      v.t1[i] = b[i] - v.t1[i];
+      rn = fmax(rn, fabs(v.t1[i]));
+    }
+    rn = ex.max(rn);
+    ex.sync();
+    if (rn < 1e-15 * fmax(1.0, bn)) break;
+    bqp_ldl_solve(ex, d, v.Lb, v.t1, v.t2);
+    for (int i = ex.lane; i < d.nk; i += ex.nlanes) out[i] += v.t2[i];
+    ex.sync();
+  }
+}
+
+// largest step in (0, 1] keeping s + a ds >= 0 and z + a dz >= 0 over the inequality rows
+template <class X>
+BMPC_HD double bqp_step(const X& ex, const BandQPDesc& d, const BandQPWs& v) {
+  double a = 1.0;
+  for (int i = ex.lane; i < d.nk; i += ex.nlanes) {
+    if (d.kind[i] != QPK_IN) continue;
+    if (v.ds[i] < 0) a = fmin(a, -v.s[i] / v.ds[i]);
+    if (v.dw[i] < 0) a = fmin(a, -v.w[i] / v.dw[i]);
+  }
+  return ex.min(a);
+}
+
+// One problem.  vals = [Px; Ax], cvals = [q; l; u] (the CSC value arrays of the shared
+// pattern); x [n], y [m] (OSQP's dual: P x + q + A'y = 0); returns the QP_* status.
+template <class X>
+BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
+                         double* x, double* y, int* iters) {
+  const int nk = d.nk, nl = ex.nlanes, lane = ex.lane;
+  const BandQPWs v = bandqp_ws(d, ws);
+  const double rs = 1e-8;   // static regularisation (ECOS's STATIC_REG)
+  // ---- assemble the band and the right-hand-side constants c (q | e | g by row kind)
+  for (size_t t = lane; t < (size_t)nk * d.W; t += nl) v.Kb[t] = 0.0;
+  for (int i = lane; i < nk; i += nl) v.c[i] = 0.0;
+  ex.sync();
+  for (int t = lane; t < d.nscat; t += nl) v.Kb[d.scat[3 * t + 1]] = d.scat[3 * t + 2] * vals[d.scat[3 * t]];
+  for (int t = lane; t < d.ncscat; t += nl) v.c[d.cscat[3 * t + 1]] = d.cscat[3 * t + 2] * cvals[d.cscat[3 * t]];
+  ex.sync();
+  double nq = 0.0, ne = 0.0, ng = 0.0;
+  for (int i = lane; i < nk; i += nl) {
+    const int kd = d.kind[i];
+    const double a = fabs(v.c[i]);
+    if (kd == QPK_X) nq = fmax(nq, a); else if (kd == QPK_EQ) ne = fmax(ne, a); else ng = fmax(ng, a);
+  }
+  nq = fmax(1.0, ex.max(nq));
+  ne = fmax(1.0, ex.max(ne));
+  ng = fmax(1.0, ex.max(ng));
+
+  // ---- initial point: solve with S/Z = I, then shift s into the interior (oracle/qp_ipm.py:51-56)
+  for (int i = lane; i < nk; i += nl) {
+    const int kd = d.kind[i];
+    const double pd = kd == QPK_X ? v.Kb[(size_t)i * d.W] : 0.0;
+    v.tdg[i] = kd == QPK_X ? pd : (kd == QPK_EQ ? 0.0 : -1.0);
+    v.fdg[i] = kd == QPK_X ? pd + rs : v.tdg[i] - rs;
+    v.rhs[i] = kd == QPK_X ? -v.c[i] : v.c[i];
+  }
+  ex.sync();
+  bqp_factor(ex, d, v.Kb, v.fdg, v.Lb);
+  bqp_solve_refined(ex, d, v, v.rhs, v.w);
+  for (int i = lane; i < nk; i += nl) {
+    v.t2[i] = d.kind[i] == QPK_X ? v.w[i] : 0.0;
+    v.fdg[i] = d.kind[i] == QPK_X ? v.Kb[(size_t)i * d.W] : 0.0;   // diagonal of [P E' G'; E 0 0; G 0 0]
+  }
+  ex.sync();
+  bqp_matvec(ex, d, v.Kb, v.fdg, v.t2, v.r);   // z rows: G x
+  double smin = 1e300;
+  for (int i = lane; i < nk; i += nl)
+    if (d.kind[i] == QPK_IN) {
+      v.s[i] = v.c[i] - v.r[i];
+      smin = fmin(smin, v.s[i]);
+    } else {
+      v.s[i] = 0.0;
+    }
+  smin = ex.min(smin);
+  const double shift = (d.n_in > 0 ? fmax(0.0, -smin) : 0.0) + 1.0;
+  for (int i = lane; i < nk; i += nl)
+    if (d.kind[i] == QPK_IN) {
+      v.s[i] += shift;
+      v.w[i] = fmax(fabs(v.w[i]), 1.0);
+    }
+  ex.sync();
+
+  int status = QP_MAX_ITER, it = 0;
+  const double inv_m = d.n_in > 0 ? 1.0 / d.n_in : 0.0;
+  for (it = 0; it < d.max_iter; ++it) {
+    // ---- residuals: rd = Px + q + E'y + G'z, re = Ex - e, rg = Gx + s - g, mu
+    for (int i = lane; i < nk; i += nl) v.fdg[i] = d.kind[i] == QPK_X ? v.Kb[(size_t)i * d.W] : 0.0;
+    ex.sync();
+    bqp_matvec(ex, d, v.Kb, v.fdg, v.w, v.r);
+    double rd = 0.0, re = 0.0, rg = 0.0, sz = 0.0;
+    for (int i = lane; i < nk; i += nl) {
+      const int kd = d.kind[i];
+      if (kd == QPK_X) {
+        v.r[i] += v.c[i];
+        rd = fmax(rd, fabs(v.r[i]));
+      } else if (kd == QPK_EQ) {
+        v.r[i] -= v.c[i];
+        re = fmax(re, fabs(v.r[i]));
+      } else {
+        v.r[i] += v.s[i] - v.c[i];
+        rg = fmax(rg, fabs(v.r[i]));
+        sz += v.s[i] * v.w[i];
+      }
+    }
+    rd = ex.max(rd);
+    re = ex.max(re);
+    rg = ex.max(rg);
+    const double mu = ex.sum(sz) * inv_m;
+    ex.sync();
+    if (!(rd == rd) || !(mu == mu) || !(rg == rg) || !(re == re)) {
+      status = QP_NUMERICS;
+      break;
+    }
+    if (rd < d.eps * nq && re < d.eps * ne && rg < d.eps * ng && mu < d.eps) {
+      status = QP_SOLVED;
+      break;
+    }
+    // ---- factor the Newton matrix (diagonal -S/Z on the inequality rows)
+    for (int i = lane; i < nk; i += nl) {
+      const int kd = d.kind[i];
+      const double pd = kd == QPK_X ? v.Kb[(size_t)i * d.W] : 0.0;
+      v.tdg[i] = kd == QPK_X ? pd : (kd == QPK_EQ ? 0.0 : -v.s[i] / v.w[i]);
+      v.fdg[i] = kd == QPK_X ? pd + rs : v.tdg[i] - rs;
+      v.rhs[i] = kd == QPK_IN ? -v.r[i] + v.s[i] : -v.r[i];
+    }
+    ex.sync();
+    bqp_factor(ex, d, v.Kb, v.fdg, v.Lb);
+    // ---- predictor (affine) step
+    bqp_solve_refined(ex, d, v, v.rhs, v.dw);
+    for (int i = lane; i < nk; i += nl)
+      v.ds[i] = d.kind[i] == QPK_IN ? -v.s[i] - v.s[i] / v.w[i] * v.dw[i] : 0.0;
+    ex.sync();
+    const double aa = bqp_step(ex, d, v);
+    double sa = 0.0;
+    for (int i = lane; i < nk; i += nl)
+      if (d.kind[i] == QPK_IN) sa += (v.s[i] + aa * v.ds[i]) * (v.w[i] + aa * v.dw[i]);
+    const double mua = ex.sum(sa) * inv_m;
+    const double sig = mu > 0 ? (mua / mu) * (mua / mu) * (mua / mu) : 0.0;
+    // ---- corrector: rhs of the inequality rows gains (ds dz - sig mu) / z; t2 keeps that term
+    for (int i = lane; i < nk; i += nl)
+      if (d.kind[i] == QPK_IN) {
+        const double corr = (v.ds[i] * v.dw[i] - sig * mu) / v.w[i];
+        v.t2[i] = corr;
+        v.rhs[i] += corr;
+      }
+    ex.sync();
+    // t2 is the refinement scratch: stash corr in ds first
+    for (int i = lane; i < nk; i += nl) v.ds[i] = d.kind[i] == QPK_IN ? v.t2[i] : 0.0;
+    ex.sync();
+    bqp_solve_refined(ex, d, v, v.rhs, v.dw);
+    for (int i = lane; i < nk; i += nl)
+      if (d.kind[i] == QPK_IN) v.ds[i] = -v.s[i] - v.s[i] / v.w[i] * v.dw[i] - v.ds[i];
+    ex.sync();
+    const double a = 0.99 * bqp_step(ex, d, v);
+    for (int i = lane; i < nk; i += nl) {
+      v.w[i] += a * v.dw[i];
+      if (d.kind[i] == QPK_IN) v.s[i] += a * v.ds[i];
+    }
+    ex.sync();
+  }
+  for (int j = lane; j < d.n; j += nl) x[j] = v.w[d.xmap[j]];
+  for (int r = lane; r < d.m; r += nl) {
+    const int32_t* ym = d.ymap + 4 * r;
+    double yr = 0.0;
+    if (ym[0] >= 0) yr += ym[1] * v.w[ym[0]];
+    if (ym[2] >= 0) yr += ym[3] * v.w[ym[2]];
+    y[r] = yr;
+  }
+  if (iters && lane == 0) *iters = it;
+  ex.sync();
+  return status;
+}
+
+}  // namespace bmpc

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -17,6 +18,7 @@
 #include "bmpc_env.h"
 #include "bmpc_hmm.h"
 #include "bmpc_qp.h"
+#include "bmpc_qpplan.h"
 #include "bmpc_solve.h"
 
 using namespace bmpc;
@@ -240,6 +242,19 @@ __global__ void k_hmm(int M, int m, const double* __restrict__ hc, int B, const 
   hmm_linearize(M, m, hc, xb + (size_t)p * nb, u + (size_t)p * 2, xbackup + (size_t)p * M * m * 4, OFF(xbp, nb),
                 OFF(A, nb * nb), OFF(Bm, nb * 2), OFF(C, nb), OFF(h0, M * m), OFF(Jh, M * m * nb));
 #undef OFF
+}
+
+// one wave per QP of the batch (bmpc_bandqp.h); d's tables are device pointers
+__global__ __launch_bounds__(64) void k_bandqp(BandQPDesc d, const double* __restrict__ vals,
+                                               const double* __restrict__ cvals, double* __restrict__ ws,
+                                               double* x, double* y, int32_t* status, int32_t* iters, int batch) {
+  const int b = blockIdx.x;
+  if (b >= batch) return;
+  extern __shared__ double lds_dyn[];
+  const DevExec ex{(int)threadIdx.x, (ldouble*)lds_dyn, nullptr, nullptr};
+  const int st = bandqp_solve(ex, d, vals + (size_t)b * d.nvals, cvals + (size_t)b * d.ncvals, ws + d.stride * b,
+                              x + (size_t)b * d.n, y + (size_t)b * d.m, iters ? iters + b : nullptr);
+  if (threadIdx.x == 0) status[b] = st;
 }
 
 thread_local std::string g_err;
@@ -833,6 +848,68 @@ int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const do
   HIPCHECK(hipDeviceSynchronize());
   for (int i = 0; i < 6; ++i)
     if (out_h[i]) HIPCHECK(hipMemcpy(out_h[i], dout[i], (size_t)B * out_sz[i] * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                  const int32_t* Ai, int batch, const double* Px, const double* q, const double* Ax, const double* l,
+                  const double* u, int max_iter, double eps, double* x, double* y, int32_t* status, int32_t* iters,
+                  int32_t* info) {
+  if (!ctx || !q || !x || !status) return fail(-22, "null argument");
+  HostBandQP h;
+  std::string err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, h);
+  if (!err.empty()) return fail(-22, err);
+  const int nnzP = Pp[n], nnzA = Ap[n];
+  if ((nnzP && !Px) || (nnzA && !Ax)) return fail(-22, "null value array");
+  if (info) {
+    info[0] = h.d.nk;
+    info[1] = h.d.bw;
+    info[2] = h.d.n_in;
+    info[3] = h.d.nscat;
+  }
+  HIPCHECK(hipSetDevice(ctx->device));
+  const size_t B = (size_t)batch;
+  // host values in the kernel's per-problem order: [Px; Ax] and [q; l; u]
+  std::vector<double> vals(B * h.d.nvals), cvals(B * h.d.ncvals);
+  for (size_t b = 0; b < B; ++b) {
+    double* v = vals.data() + b * h.d.nvals;
+    if (nnzP) memcpy(v, Px + b * nnzP, nnzP * sizeof(double));
+    if (nnzA) memcpy(v + nnzP, Ax + b * nnzA, nnzA * sizeof(double));
+    double* c = cvals.data() + b * h.d.ncvals;
+    memcpy(c, q + b * n, n * sizeof(double));
+    if (m) {
+      memcpy(c + n, l + b * m, m * sizeof(double));
+      memcpy(c + n + m, u + b * m, m * sizeof(double));
+    }
+  }
+  DevBuf dtab, dvals, dcvals, dws, dout;
+  HIPCHECK(upload(dtab, h.blob.data(), h.blob.size() * sizeof(int32_t)));
+  HIPCHECK(upload(dvals, vals.data(), std::max<size_t>(vals.size(), 1) * sizeof(double)));
+  HIPCHECK(upload(dcvals, cvals.data(), cvals.size() * sizeof(double)));
+  HIPCHECK(dws.alloc(B * h.d.stride * sizeof(double)));
+  const size_t nout = B * (n + m) * sizeof(double) + 2 * B * sizeof(int32_t);
+  HIPCHECK(dout.alloc(nout));
+  double* dx = dout.as<double>();
+  double* dy = dx + B * n;
+  int32_t* dst = reinterpret_cast<int32_t*>(dy + B * m);
+  int32_t* dit = dst + B;
+  BandQPDesc d = h.d;
+  const int32_t* base = dtab.as<int32_t>();
+  d.kind = base;
+  d.scat = d.kind + h.kind.size();
+  d.cscat = d.scat + h.scat.size();
+  d.xmap = d.cscat + h.cscat.size();
+  d.ymap = d.xmap + h.xmap.size();
+  const size_t lds = bandqp_lds_doubles(d.nk, d.W) * sizeof(double);
+  if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute((const void*)k_bandqp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_bandqp, dim3(batch), dim3(64), lds, 0, d, dvals.as<double>(), dcvals.as<double>(),
+                     dws.as<double>(), dx, dy, dst, dit, batch);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipMemcpy(x, dx, B * n * sizeof(double), hipMemcpyDeviceToHost));
+  if (y && m) HIPCHECK(hipMemcpy(y, dy, B * m * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(status, dst, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (iters) HIPCHECK(hipMemcpy(iters, dit, B * sizeof(int32_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -268,6 +268,26 @@ int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const do
                   const double* xbackup, double* xbp, double* A, double* Bm, double* C, double* h0,
                   double* Jh);
 
+/* Batched convex QP in OSQP's problem form (the solver behind the belief LTV-MPC,
+ * PredictiveControllers.MPC.osqp_solve_qp, PredictiveControllers.py:310-340, which the
+ * reference hands to OSQP(...).setup(P, q, A, l, u, polish=True).solve()):
+ *     minimise 1/2 x'Px + q'x  subject to  l <= A x <= u
+ * by a Mehrotra interior-point method on the quasidefinite KKT matrix, band-factored after a
+ * reverse Cuthill-McKee ordering, one wave per problem (csrc/bmpc_bandqp.h).  The problems of
+ * a batch share one sparsity pattern:
+ *   Pp [n+1], Pi [nnzP]      upper triangle of P, CSC (OSQP keeps only the upper triangle)
+ *   Ap [n+1], Ai [nnzA]      A (m x n), CSC; row indices increasing within a column
+ *   Px [batch][nnzP], Ax [batch][nnzA], q [batch][n], l, u [batch][m]
+ * |bound| >= 1e20 is infinite; a row with l == u is an equality; every problem must classify
+ * every row alike.  Outputs: x [batch][n]; y [batch][m] (OSQP's dual, P x + q + A'y = 0;
+ * NULL skips); status [batch] (1 solved to eps, -2 max_iter reached, -8 numerical failure);
+ * iters [batch] (NULL skips); info [4] = {KKT dimension, bandwidth, inequality rows, band
+ * entries} (NULL skips).  -22 when the KKT band does not fit the 160 KB LDS window. */
+int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                  const int32_t* Ai, int batch, const double* Px, const double* q, const double* Ax, const double* l,
+                  const double* u, int max_iter, double eps, double* x, double* y, int32_t* status, int32_t* iters,
+                  int32_t* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,7 @@
 #include "bmpc_hmm.h"
 #include "bmpc_solve.h"
 #include "bmpc_env.h"
+#include "bmpc_qpplan.h"
 
 using namespace bmpc;
 
@@ -269,6 +270,39 @@ int hs_hmm_eval(int M, int m, const double* hc, int B, const double* xb, const d
                   xbp ? xbp + (size_t)p * nb : nullptr, A ? A + (size_t)p * nb * nb : nullptr,
                   Bm ? Bm + (size_t)p * nb * 2 : nullptr, C ? C + (size_t)p * nb : nullptr,
                   h0 ? h0 + (size_t)p * M * m : nullptr, Jh ? Jh + (size_t)p * M * m * nb : nullptr);
+  return 0;
+}
+
+int hs_qp_solve(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap, const int32_t* Ai, int batch,
+                const double* Px, const double* q, const double* Ax, const double* l, const double* u, int max_iter,
+                double eps, double* x, double* y, int32_t* status, int32_t* iters, int32_t* info) {
+  HostBandQP h;
+  g_err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, h);
+  if (!g_err.empty()) return -22;
+  if (info) {
+    info[0] = h.d.nk;
+    info[1] = h.d.bw;
+    info[2] = h.d.n_in;
+    info[3] = h.d.nscat;
+  }
+  const int nnzP = Pp[n], nnzA = Ap[n];
+  std::vector<double> vals(h.d.nvals + 1), cvals(h.d.ncvals), ws(h.d.stride), lds(bandqp_lds_doubles(h.d.nk, h.d.W));
+  std::vector<double> ybuf(m + 1);
+  HostExec ex;
+  ex.lds = lds.data();
+  for (int b = 0; b < batch; ++b) {
+    for (int t = 0; t < nnzP; ++t) vals[t] = Px[(size_t)b * nnzP + t];
+    for (int t = 0; t < nnzA; ++t) vals[nnzP + t] = Ax[(size_t)b * nnzA + t];
+    for (int j = 0; j < n; ++j) cvals[j] = q[(size_t)b * n + j];
+    for (int r = 0; r < m; ++r) {
+      cvals[n + r] = l[(size_t)b * m + r];
+      cvals[n + m + r] = u[(size_t)b * m + r];
+    }
+    int it = 0;
+    status[b] = bandqp_solve(ex, h.d, vals.data(), cvals.data(), ws.data(), x + (size_t)b * n,
+                             y ? y + (size_t)b * m : ybuf.data(), &it);
+    if (iters) iters[b] = it;
+  }
   return 0;
 }
 

@@ -24,7 +24,8 @@ from bmpc import abi  # noqa: E402
 FLAGS = os.environ.get("BMPC_HOSTSIM_FLAGS", "").split()
 SO = os.path.join(HERE, "hostsim", "libbmpc_hostsim%s.so" % (
     "" if not FLAGS else "_" + "".join(c if c.isalnum() else "_" for c in "".join(FLAGS))[:80]))
-SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", "bmpc_plan.cpp")]
+SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", "bmpc_plan.cpp"),
+        os.path.join(PKG, "csrc", "bmpc_qpplan.cpp")]
 HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")]
 
 
@@ -173,3 +174,21 @@ def hmm_eval(M, m, consts, xb, u, xbackup):
                h0=np.zeros((B, M, m)), Jh=np.zeros((B, M, m, nb)))
     lib().hs_hmm_eval(M, m, _p(hc), B, _p(xb), _p(u), _p(xbk), *(_p(out[k]) for k in ("xbp", "A", "B", "C", "h0", "Jh")))
     return out
+
+
+def qp_solve(n, m, Pp, Pi, Ap, Ai, Px, q, Ax, l, u, max_iter=100, eps=1e-10):
+    """Host build of bmpc_qp_solve (batched arrays: Px [B][nnzP], q [B][n], ...)."""
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)
+    f64 = lambda a: np.ascontiguousarray(a, float)
+    Pp, Pi, Ap, Ai = i32(Pp), i32(Pi), i32(Ap), i32(Ai)
+    q = f64(q).reshape(-1, n)
+    B = q.shape[0]
+    Px, Ax = f64(Px).reshape(B, -1), f64(Ax).reshape(B, -1)
+    l, u = f64(l).reshape(B, m), f64(u).reshape(B, m)
+    x, y = np.zeros((B, n)), np.zeros((B, m))
+    st, it, info = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(4, np.int32)
+    rc = lib().hs_qp_solve(n, m, _p(Pp), _p(Pi), _p(Ap), _p(Ai), B, _p(Px), _p(q), _p(Ax), _p(l), _p(u),
+                           int(max_iter), C.c_double(eps), _p(x), _p(y), _p(st), _p(it), _p(info))
+    if rc != 0:
+        raise RuntimeError(lib().hs_last_error().decode())
+    return dict(x=x, y=y, status=st, iters=it, info=info)

@@ -498,6 +498,98 @@ def gen_merge(name, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+def belief_scene_step(x, z, u, true_j, xbackup, m, dt):
+    """The recording's scene (not the reference's: Highway_env.py, its only caller, is dead
+    code): the ego integrates its input with Highway_env.vehicle.step's Euler rule (:40-42);
+    agent i moves to the first state of its backup rollout under its true policy."""
+    x = x + dt * np.array([x[2] * np.cos(x[3]), x[2] * np.sin(x[3]), u[0], u[1]])
+    z = [xbackup[m * i + true_j[i], 0:4].copy() for i in range(len(z))]
+    return x, z
+
+
+def belief_next(xpred1, nx, M, m):
+    """Next beliefs: the MPC's own one-step belief prediction, read row-major as it reads
+    them (:208), clipped at 0 and renormalised per agent."""
+    b = np.maximum(np.reshape(np.asarray(xpred1[nx:], float), (M, m)), 0.0) + 1e-9
+    return b / b.sum(axis=1, keepdims=True)
+
+
+def gen_belief(name, M, m, N, z0, true_j, steps, keep, out):
+    """PredictiveControllers.MPC (:56-340), the reference's own class over the reference's
+    own HMM model (HMM_backup_dyn.py over the CasADi shim, its backup_maintain / backup_brake
+    and a constant -2 m/s^2 brake as the third policy), parameters from the reference's
+    Init_MPC.initMPCParams (:7-34).  get_xLin :121 raises TypeError as shipped; the recording
+    subclass replaces only that line's np.reshape(b0, -1, 1) by np.reshape(b0, -1).  OSQP is
+    the oracle QP interior point behind the stub (install_stubs)."""
+    from gen_golden_model import import_reference_models
+    _, _, HM, utils = import_reference_models()
+    import Init_MPC
+    import PredictiveControllers as RPC
+    assert os.path.dirname(os.path.abspath(RPC.__file__)) == REF
+
+    class FixedMPC(RPC.MPC):
+        def get_xLin(self, x0, xbackup, b0):
+            if self.uLin is None:
+                self.uLin = np.zeros([self.N, self.d])
+            self.uLin = np.vstack((self.uLin, self.uLin[-1]))
+            self.xLin = np.zeros([self.N + 1, self.n])
+            xb = np.append(x0, np.reshape(b0, -1))
+            self.xLin[0] = xb
+            for i in range(0, self.N):
+                A, B, C, h0, Jh = self.predictiveModel.regressionAndLinearization(
+                    xb, xbackup[:, i * self.nx:(i + 1) * self.nx], self.uLin[i])
+                xbp = C + A.dot(xb) + B.dot(self.uLin[i])
+                self.xLin[i + 1] = xbp
+                xb = xbp
+
+    cons = utils.Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=6.0, rm=0.3, J_c=20, s_c=1,
+                                  ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    pols = [lambda x: HM.backup_maintain(x, cons), lambda x: HM.backup_brake(x, cons),
+            lambda x: np.array([-2.0, -cons.Kpsi * x[3]])][:m]
+    dt, nx, N_lane, ydes, vdes = 0.1, 4, 2, 1.8, 15.0
+    model = HM.PredictiveModel(nx, 2, M, pols, dt, cons)
+    param = Init_MPC.initMPCParams(nx, 2, N, M, m, ydes, vdes, cons.am, cons.rm, N_lane, cons.W)
+    mpc = FixedMPC(param, model)
+    x = np.array([0.0, 1.8, 15.0, 0.0])
+    z = [np.array(v, float) for v in z0]
+    b = np.ones([M, m]) / m
+    xRef = np.array([0.0, ydes, vdes, 0.0])
+    d_out = dict(M=M, m=m, N=N, nx=nx, dt=dt, N_lane=N_lane, ydes=ydes, vdes=vdes, am=cons.am, rm=cons.rm,
+                 W=cons.W, true_j=np.array(true_j), hc=np.array([dt, cons.L, cons.W, cons.ylb, cons.yub,
+                                                                 cons.col_alpha, cons.s1, cons.tran_diag]))
+    traj = {k: [] for k in ("x", "z", "b", "xbackup", "uLin_in", "old_in", "u", "status", "sol", "slackdim")}
+    for t in range(steps):
+        xbackup = np.array(model.generate_backup_traj(np.array(z), N), float)
+        traj["uLin_in"].append(np.full((N + 1, 2), np.nan) if mpc.uLin is None else
+                               np.vstack((mpc.uLin, np.full((N + 1 - len(mpc.uLin), 2), np.nan))))
+        traj["old_in"].append(np.asarray(mpc.OldInput, float).reshape(-1))
+        for k, v in (("x", x), ("z", np.array(z)), ("b", b), ("xbackup", xbackup)):
+            traj[k].append(np.array(v, float))
+        mpc.solve(x, b, xbackup, xRef)
+        prob, sol, info, kw = CURRENT["captured"]
+        traj["u"].append(np.array(mpc.uPred[0], float))
+        traj["status"].append(info["status_val"])
+        traj["sol"].append(np.array(sol, float))
+        traj["slackdim"].append(mpc.slackdim)
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.P, p + "P", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "q"], d_out[p + "l"], d_out[p + "u"] = prob.q, prob.l, prob.u
+            d_out[p + "xLin"] = np.array(mpc.xPred, float)   # (kept for the record)
+            d_out[p + "uPred"] = np.array(mpc.uPred, float)
+        print(f"[{name}] t={t:3d} status={info['status_val']} it={info['iter']:3d} rows={mpc.slackdim} "
+              f"u0={mpc.uPred[0]}", flush=True)
+        x, z = belief_scene_step(x, z, mpc.uPred[0], true_j, xbackup, m, dt)
+        b = belief_next(mpc.xPred[1], nx, M, m)
+    L = max(len(v) for v in traj["sol"])
+    traj["sol"] = [np.append(v, np.full(L - len(v), np.nan)) for v in traj["sol"]]
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -517,6 +609,9 @@ def main():
         "highway_robust_n8_nb2": lambda: gen_highway_robust("highway_robust_n8_nb2", 8, 2, 5 if a.quick else 20, {0, 1, 10}, out),
         "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
         "merge_n40_nb1": lambda: gen_merge("merge_n40_nb1", 4 if a.quick else 60, {0, 1, 2, 30, 45}, out),
+        "belief_m1": lambda: gen_belief("belief_m1", 1, 3, 10, [[10.0, 1.8, 12.0, 0.0]], [1], 12, {0, 1, 6}, out),
+        "belief_m2": lambda: gen_belief("belief_m2", 2, 2, 8, [[12.0, 1.8, 12.0, 0.0], [-6.0, 5.4, 17.0, 0.0]], [1, 0],
+                                        10, {0, 4}, out),
     }
     for k, f in jobs.items():
         if a.only and k not in a.only.split(","):
