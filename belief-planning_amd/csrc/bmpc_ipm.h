@@ -1696,7 +1696,6 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   const double resy0 = fmax(1.0, sqrt(vdot(ex, bv, bv, neq)));
   const double resz0 = fmax(1.0, sqrt(vdot(ex, hv, hv, nr)));
   double best_score = 1e300, best_tau = 1.0;
-  int stall = 0;
   int best_it = 0;
   BMPC_TOC(ws, L, PROF_INIT, t_init);
   double bs_pres = 0, bs_dres = 0, bs_relgap = 0, bs_gap = 0, bs_pcost = 0;
@@ -1780,9 +1779,6 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       return 99;
     };
     const double score = fmax(fmax(pres, dres), relgap >= 0.0 ? relgap : 1e300);
-    // stall counter: only in the end game (best iterate within the inaccurate tolerances)
-    if (score < 0.5 * best_score || best_score > 1e-4) stall = 0;
-    else ++stall;
     if (score < best_score) {
       best_score = score;
       best_it = it;
@@ -1797,30 +1793,16 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     if (blockIdx.x == 0 && ex.lane == 0)
 #endif
     printf("it %3d pcost %+.9e dcost %+.9e gap %.2e pres %.2e dres %.2e k/t %.2e tau %.2e nx %.2e ny %.2e nz %.2e ns %.2e"
-           " stall %d best %.3e maxit %d\n",
-           it, pcost, dcost, gap, pres, dres, kap / tau, tau, nx, ny, nz, ns, stall, best_score, P.desc.maxit);
+           " best %.3e maxit %d\n",
+           it, pcost, dcost, gap, pres, dres, kap / tau, tau, nx, ny, nz, ns, best_score, P.desc.maxit);
 #endif
     int code = check(feastol, abstol, reltol);
-    if (code == 99 && stall >= 5) {    // no progress for 5 end-game iterations: precision floor
-      const int c2 = check(1e-4, 5e-5, 5e-5);
-      if (c2 != 99) code = c2 + EXIT_INACC;
-      else if (best_score < 1e300) {
-        const bool inacc = bs_ok_cx && bs_pres < 1e-4 && bs_dres < 1e-4 &&
-                           (bs_gap < 5e-5 || (bs_relgap >= 0.0 && bs_relgap < 5e-5));
-        lane_batch<16>(ex, 0, nv, [&](int i) { return ws[L.bestx + i] / best_tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
-        ex.sync();
-        res.exit_flag = inacc ? EXIT_OPTIMAL + EXIT_INACC : EXIT_MAXIT;
-        res.iters = it;
-        res.pcost = bs_pcost;
-        return res;
-      }
-    }
     if (code == 99 && it == P.desc.maxit) {
       const int c2 = check(1e-4, 5e-5, 5e-5);
       code = c2 == 99 ? EXIT_MAXIT : c2 + EXIT_INACC;
     }
 #if defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__)
-    if (blockIdx.x == 0 && ex.lane == 0) printf("   code %d (it %d, stall %d)\n", code, it, stall);
+    if (blockIdx.x == 0 && ex.lane == 0) printf("   code %d (it %d)\n", code, it);
 #endif
     if (code != 99) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] / tau; }, [&](int i, double v) { ws[L.sol + i] = v; });

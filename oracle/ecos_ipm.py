@@ -14,7 +14,9 @@ algorithm (Domahidi, Chu, Boyd, "ECOS: An SOCP solver for embedded systems", ECC
 * ECOS default tolerances (feastol = abstol = reltol = 1e-8, inaccurate 1e-4/5e-5),
   maxit = 100, step factor gamma = 0.99, and its exit codes
   (0 optimal, 1 primal infeasible, 2 dual infeasible, 10+ inaccurate, -1 maxit,
-  -2 numerics).
+  -2 numerics): optimal at the full tolerances; at maxit, or when a step fails
+  numerically (ECOS backtracks to its best iterate), inaccurate if the best iterate meets
+  the reduced tolerances, else -1 / -2.  No other early exit.
 
 Linear algebra is a sparse LU of the full KKT matrix
 ``[[0, A', G'], [A, 0, 0], [G, 0, -W'W]]`` (ECOS uses a sparse LDL' with static
@@ -376,7 +378,6 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
     resz0 = max(1.0, np.linalg.norm(h))
     info = dict(exitFlag=ECOS_MAXIT, iter=0)
     best = None          # (score, iterate, stats)
-    stall = 0
 
     def pack(code, it, st, xs, ys, zs, ss, ts):
         info.update(st, exitFlag=code, iter=it)
@@ -433,23 +434,10 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
 
         # ECOS safeguard: remember the best iterate by its worst residual
         score = max(pres, dres, relgap if not np.isnan(relgap) else np.inf)
-        # stall counter: only in the end game (best iterate already meets the inaccurate
-        # tolerances), iterations that do not halve the best score
-        stall = 0 if (best is None or score < 0.5 * best[0] or best[0] > FEASTOL_INACC) else stall + 1
         if best is None or score < best[0]:
             best = (score, it, stats, x.copy(), y.copy(), z.copy(), s.copy(), tau)
 
         code = exit_check(feastol, abstol, reltol)
-        if code is None and stall >= 5:         # no progress for 5 end-game iterations
-            code2 = exit_check(FEASTOL_INACC, ABSTOL_INACC, RELTOL_INACC)
-            if code2 is not None:
-                code = code2 + ECOS_INACC_OFFSET
-            else:
-                _, bit, bst, bx_, by_, bz_, bs_, btau = best
-                ok = (bst['pres'] < FEASTOL_INACC and bst['dres'] < FEASTOL_INACC and
-                      (bst['gap'] < ABSTOL_INACC or (not np.isnan(bst['relgap']) and bst['relgap'] < RELTOL_INACC)))
-                return pack(ECOS_OPTIMAL + ECOS_INACC_OFFSET if ok else ECOS_MAXIT, it, bst,
-                            bx_, by_, bz_, bs_, btau)
         if code is None and it == maxit:
             code2 = exit_check(FEASTOL_INACC, ABSTOL_INACC, RELTOL_INACC)
             code = ECOS_MAXIT if code2 is None else code2 + ECOS_INACC_OFFSET

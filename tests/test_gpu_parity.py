@@ -89,7 +89,7 @@ def test_batch_matches_host_build(gpu):
         # (1e-6; the two builds sum in different orders, observed up to 2e-7); otherwise ECOS
         # "inaccurate" class (1e-4 gap)
         tight = (r["status"] == 0) & (h["status"] == 0)
-        assert np.mean(r["status"] == h["status"]) >= 0.8   # 0 vs 10 is decided at the rounding floor
+        assert np.mean(r["status"] == h["status"]) >= 0.9   # 0 vs 10 is decided at the rounding floor
         np.testing.assert_allclose(r["J"][tight], h["J"][tight], rtol=1e-6)
         np.testing.assert_allclose(r["upred"][tight, 0], h["upred"][tight, 0], atol=1e-5)
         np.testing.assert_allclose(r["J"], h["J"], rtol=1e-4)

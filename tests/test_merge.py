@@ -42,13 +42,16 @@ def replay_inputs(g, steps=None):
 
 
 def check_merge_replay(r, g, T):
-    """Tolerances: J to 1e-6 relative (exit 0); uPred[0] to 5e-4.  The merge cost is
+    """Exit codes agree on >= 85% of the steps.  Tolerances: J to 1e-6 relative (exit 0);
+    uPred[0] to 5e-4.  The merge cost is
     ~3e4, so ECOS's 1e-8 relative gap fixes J to ~3e-4 absolute, and through the input cost
     (R = diag(1, 100)) that only pins u to ~1e-2; late in the scene (u ~ 1e-2) the recorded
     and the kernel's optima differ by up to ~1.2e-4 in the acceleration."""
     exits, J, u = (np.asarray(g[k][:T]) for k in ("traj_exit", "traj_J", "traj_u"))
     assert np.all(r["status"] >= 0), r["status"]
-    assert np.mean(r["status"] == exits) >= 0.8, (r["status"], exits)
+    # exit 0 vs 10 at the rounding floor: the merge cost (~4e4) puts ECOS's 1e-8 gap at the
+    # precision floor of the structured KKT solve on ~1 step in 9 (53 of 60 agree)
+    assert np.mean(r["status"] == exits) >= 0.85, (r["status"], exits)
     for t in range(T):
         tight = exits[t] == 0 and r["status"][t] == 0
         rtol, atol = (1e-6, 5e-4) if tight else (1e-4, 5e-3)
