@@ -196,7 +196,8 @@ typedef const BMPC_AS_CONST Plan CPlan;
 typedef const BMPC_AS_CONST Layout CLayout;
 
 // misc slots
-enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */, MISC_X0 = 8 /* n values (robustMPC) */ };
+enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */, MISC_BEST = 6 /* best score, its tau (IPM guard) */,
+       MISC_X0 = 8 /* n values (robustMPC) */ };
 
 
 

@@ -67,6 +67,9 @@ struct DevExecT {
     return v;
   }
   __device__ void sync() const { __syncthreads(); }
+  // a wave-uniform flag as a scalar: branches on it (and the calls they guard) run with the
+  // full exec mask instead of an exec mask derived from a VGPR the compiler cannot prove uniform
+  __device__ bool uniform(bool b) const { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
   __device__ double sum(double v) const {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -56,7 +56,8 @@ namespace bmpc {
 
 enum {
   EXIT_OPTIMAL = 0, EXIT_PINF = 1, EXIT_DINF = 2, EXIT_INACC = 10,
-  EXIT_MAXIT = -1, EXIT_NUMERICS = -2
+  EXIT_MAXIT = -1, EXIT_NUMERICS = -2,
+  EXIT_GUARD = -9   // internal consistency guard tripped (never expected; tests assert status >= 0)
 };
 
 // ------------------------------------------------------------------------------------
@@ -1785,6 +1786,10 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       best_tau = tau;
       bs_pres = pres, bs_dres = dres, bs_relgap = relgap, bs_gap = gap, bs_pcost = pcost;
       bs_ok_cx = (-cx > 0.0 || -by - hz >= -5e-5);
+      if (ex.lane == 0) {   // mirror for the guard below
+        ws[L.misc + MISC_BEST] = best_score;
+        ws[L.misc + MISC_BEST + 1] = best_tau;
+      }
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i]; }, [&](int i, double v) { ws[L.bestx + i] = v; });
       ex.sync();
     }
@@ -1813,8 +1818,11 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       return res;
     }
     // ---- Newton step ---------------------------------------------------------------------
-    bool ok = compute_scaling(ex, C, s, z);
-    if (ok) ok = kkt_factor<X, NX, NU>(ex, C) && kkt_coupling<X, NX, NU>(ex, C);
+    // the phase results are wave-uniform (each ends in a wave reduction); ex.uniform makes the
+    // branches scalar, so no phase is ever called under a partial exec mask
+    bool ok = ex.uniform(compute_scaling(ex, C, s, z));
+    if (ok) ok = ex.uniform(kkt_factor<X, NX, NU>(ex, C));
+    if (ok) ok = ex.uniform(kkt_coupling<X, NX, NU>(ex, C));
     double alpha = 0.0, dtau = 0.0, dkap = 0.0;
     // refinement only once the iterate nears the tolerances: an unrefined direction is
     // accurate to ~1e-12 relative, far below what the early steps need
@@ -1882,7 +1890,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
       apply_W(ex, C, 0, ds, rb);                               // ds = W dsW
       const double fin = ex.max(nonfinite);
-      ok = fin == 0.0 && isfinite(dtau) && alpha > 1e-10;
+      ok = ex.uniform(fin == 0.0 && isfinite(dtau) && alpha > 1e-10);
       if (ok) {
         lane_batch<8>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
         lane_batch(ex, 0, neq, [&](int i) { return y[i] + (alpha * y2[i]); }, [&](int i, double v) { y[i] = v; });
@@ -1895,6 +1903,14 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       }
     }
     if (!ok) {   // numerical failure: ECOS backtracks to the best iterate
+      // guard: the best iterate's score and tau are held in registers across every phase call
+      // of the loop; a build whose register allocation lost them is reported
+      // as EXIT_GUARD instead of returning a wrong point
+      if (best_score < 1e300 && (ws[L.misc + MISC_BEST] != best_score || ws[L.misc + MISC_BEST + 1] != best_tau)) {
+        res.exit_flag = EXIT_GUARD;
+        res.iters = it;
+        return res;
+      }
       const bool inacc = bs_ok_cx && bs_pres < 1e-4 && bs_dres < 1e-4 &&
                          (bs_gap < 5e-5 || (bs_relgap >= 0.0 && bs_relgap < 5e-5));
       lane_batch<16>(ex, 0, nv, [&](int i) { return ws[L.bestx + i] / best_tau; }, [&](int i, double v) { ws[L.sol + i] = v; });

@@ -30,7 +30,8 @@
  * synchronous on the plan's HIP stream unless the *_device variant is used.
  * Per-ego status follows ECOS exit codes for the CVaR controller (>= 0 means
  * "feasible", MPC_branch.py:2141) and OSQP status_val for the QP controllers
- * (1 means "feasible", MPC_branch.py:482).
+ * (1 means "feasible", MPC_branch.py:482).  CVaR status -9 is not an ECOS code: the
+ * kernel's internal consistency guard on its best-iterate state tripped (never expected).
  */
 #ifndef BMPC_H
 #define BMPC_H

@@ -35,6 +35,7 @@ struct HostExecT {
   double gmax(double v, int) const { return v; }
   double gmin(double v, int) const { return v; }
   void sync() const {}
+  bool uniform(bool b) const { return b; }
   double sum(double v) const { return v; }
   double max(double v) const { return v; }
   double min(double v) const { return v; }
