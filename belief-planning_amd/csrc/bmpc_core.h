@@ -155,11 +155,12 @@ BMPC_HD double bxv(const BMPC_AS_CONST Plan& P, const X& ex, int r) {
   else return P.desc.bx[r];
 }
 
-// LDS view of the topology tables (ex.tab = the wave's copy of the blob)
+// view of the topology tables through ex.tab: the wave's LDS copy of the blob, or the blob in
+// global memory when the copy would cost resident waves (bmpc_hip.hip, choose_topo_lds)
 #define BMPC_TOPO_SET_(n) v.n = ex.tab + P.toff[i++];
 template <class X>
-BMPC_HD TopoL topo_view(const BMPC_AS_CONST Plan& P, const X& ex) {
-  TopoL v;
+BMPC_HD TopoT<typename X::tab_ptr> topo_view(const BMPC_AS_CONST Plan& P, const X& ex) {
+  TopoT<typename X::tab_ptr> v;
   int i = 0;
   BMPC_TOPO_FIELDS(BMPC_TOPO_SET_)
   return v;

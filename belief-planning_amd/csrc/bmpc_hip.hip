@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "bmpc_plan.h"
@@ -36,12 +37,14 @@ __device__ __forceinline__ double dpp_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
-template <bool TR>
+template <bool TR, bool TL = true>
 struct DevExecT {
   static constexpr bool kTransform = TR;   // per-ego S / bx constants in LDS (merge plans)
+  // topology tables: the wave's LDS copy (TL) or the plan's blob in global memory
+  using tab_ptr = typename std::conditional<TL, lint*, gint*>::type;
   int lane;
   ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm / k_qp only)
-  lint* tab;     // this wave's LDS copy of the topology tables (k_ipm / k_qp only)
+  tab_ptr tab;   // topology tables (k_ipm / k_qp only)
   ldouble* eco;  // per-ego constants of the solve (ECO_*; kTransform only)
   static constexpr int nlanes = 64;
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
@@ -101,18 +104,31 @@ struct Bundle {
 // topology tables (Plan::ntab int32), then (transform-capable models) ECO_COUNT doubles of
 // per-ego constants.  The table copy is one batched pass at kernel start; every later tree /
 // cone / node-index lookup of the solve is an LDS read.
-__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform) {
-  const size_t tab = (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7;
+__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform, bool topo_lds) {
+  const size_t tab = topo_lds ? (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7 : 0;
   return sizeof(double) * (size_t)P.nlds + tab + (transform ? sizeof(double) * ECO_COUNT : 0);
 }
-template <bool TR>
-__device__ __forceinline__ DevExecT<TR> solver_exec(const Plan& P, double* lds_dyn) {
-  int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
+template <bool TR, bool TL>
+__device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* lds_dyn) {
   const int32_t* gtab = (const int32_t*)P.t.br_depth;   // blob base (the first table)
-  for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];
-  __syncthreads();
-  double* eco = lds_dyn + (solver_lds_bytes(P, false) / sizeof(double));
-  return DevExecT<TR>{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco};
+  double* eco = lds_dyn + (solver_lds_bytes(P, false, TL) / sizeof(double));
+  if constexpr (TL) {
+    int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
+    for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];
+    __syncthreads();
+    return DevExecT<TR, TL>{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco};
+  } else {
+    return DevExecT<TR, TL>{(int)threadIdx.x, (ldouble*)lds_dyn, (gint*)gtab, (ldouble*)eco};
+  }
+}
+
+// LDS copy of the topology tables only when it costs no resident wave: a workgroup's LDS
+// bounds the egos per CU (160 KB / bytes, at most 16 with 4 waves per SIMD), and deep trees
+// (N=30, NB=2: 17 KB of tables) would lose 3 of 7.  BMPC_TOPO_LDS=0/1 forces either.
+static bool choose_topo_lds(const Plan& P, bool transform) {
+  if (const char* e = getenv("BMPC_TOPO_LDS")) return atoi(e) != 0;
+  auto egos = [](size_t b) { return std::min<size_t>(16, (160 * 1024) / std::max<size_t>(b, 1)); };
+  return egos(solver_lds_bytes(P, transform, true)) >= egos(solver_lds_bytes(P, transform, false));
 }
 
 template <class M>
@@ -130,7 +146,7 @@ __global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, doubl
   tree_step<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
 }
 
-template <class M>
+template <class M, bool TL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm(const Bundle* __restrict__ B, double* __restrict__ ws,
                                             const bmpc_policy* __restrict__ pol, double* upred,
                                             double* xpred, double* bw, double* J, int32_t* status,
@@ -140,9 +156,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  const auto ex = solver_exec<M::kTransform>(P, lds_dyn);
+  const auto ex = solver_exec<M::kTransform, TL>(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
-  IpmResult r = solve_ego_ipm<DevExecT<M::kTransform>, M>(ex, P, L, E);
+  IpmResult r = solve_ego_ipm<DevExecT<M::kTransform, TL>, M>(ex, P, L, E);
   const double* w = E.ws;
   const int lane = threadIdx.x;
   if (upred)
@@ -158,7 +174,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   }
 }
 
-template <class M>
+template <class M, bool TL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_qp(
     const Bundle* __restrict__ B, double* __restrict__ ws, const bmpc_policy* __restrict__ pol, double* upred,
     double* xpred, double* bw, double* J, int32_t* status, int32_t* iters, int batch) {
@@ -167,9 +183,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   const Plan& P = B->P;
   const Layout& L = B->L;
   extern __shared__ double lds_dyn[];
-  const DevExec ex = solver_exec<false>(P, lds_dyn);
+  const auto ex = solver_exec<false, TL>(P, lds_dyn);
   EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
-  IpmResult r = solve_ego_qp<DevExec, M>(ex, P, L, E);
+  IpmResult r = solve_ego_qp<DevExecT<false, TL>, M>(ex, P, L, E);
   const double* w = E.ws;
   const int lane = threadIdx.x;
   if (upred)
@@ -503,7 +519,8 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
   const bool merge = P.desc.model == BMPC_MODEL_HIGHWAY_MERGE;
-  size_t lds_bytes = solver_lds_bytes(P, merge);
+  const bool tl = choose_topo_lds(P, merge);
+  size_t lds_bytes = solver_lds_bytes(P, merge, tl);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
   if (const char* e = getenv("BMPC_IPM_LDS_BYTES")) {
@@ -526,15 +543,20 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   HIPCHECK(hipGetLastError());
   if (pl->timing) HIPCHECK(hipEventRecord(ev[1], s));
   const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
-  if (P.desc.model == BMPC_MODEL_HIGHWAY)
-    hipLaunchKernelGGL(qp ? k_qp<Highway> : k_ipm<Highway>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
-                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
-  else if (merge)
-    hipLaunchKernelGGL(k_ipm<HighwayMerge>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
-                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
-  else
-    hipLaunchKernelGGL(qp ? k_qp<Quadruped> : k_ipm<Quadruped>, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle,
-                       pl->d_ws, pl->d_pol, d_upred, d_xpred, d_bw, d_J, d_status, d_iters, B);
+#define BMPC_LAUNCH_SOLVER(KERNEL)                                                                  \
+  hipLaunchKernelGGL(KERNEL, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol, d_upred, \
+                     d_xpred, d_bw, d_J, d_status, d_iters, B)
+  if (P.desc.model == BMPC_MODEL_HIGHWAY) {
+    if (tl) BMPC_LAUNCH_SOLVER((qp ? k_qp<Highway, true> : k_ipm<Highway, true>));
+    else BMPC_LAUNCH_SOLVER((qp ? k_qp<Highway, false> : k_ipm<Highway, false>));
+  } else if (merge) {
+    if (tl) BMPC_LAUNCH_SOLVER((k_ipm<HighwayMerge, true>));
+    else BMPC_LAUNCH_SOLVER((k_ipm<HighwayMerge, false>));
+  } else {
+    if (tl) BMPC_LAUNCH_SOLVER((qp ? k_qp<Quadruped, true> : k_ipm<Quadruped, true>));
+    else BMPC_LAUNCH_SOLVER((qp ? k_qp<Quadruped, false> : k_ipm<Quadruped, false>));
+  }
+#undef BMPC_LAUNCH_SOLVER
   HIPCHECK(hipGetLastError());
   if (pl->timing) {
     HIPCHECK(hipEventRecord(ev[2], s));

@@ -91,7 +91,7 @@ BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
 
 // cone-group rounds (see ConeGroups): G, and per round k / off / q of the owned cone
 #define BMPC_CONE_ROUNDS(ex, P, G)                                \
-  const TopoL G##_t = topo_view((P), ex);                         \
+  const auto G##_t = topo_view((P), ex);                         \
   const ConeGroups G = cone_groups(ex, (P).cgrp, (P).ncones);     \
   for (int rnd_ = 0; rnd_ < G.rounds; ++rnd_)
 #define BMPC_CONE_K(P, G, k, off, q)                              \
@@ -181,7 +181,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
   BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
   BMPC_COUNT(C.ws, *C.L, PROF_NAPPLYG);
   BMPC_TIC(t_glp);
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.at(C.L->dh);
   // Fx rows + positivity rows
@@ -293,7 +293,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
   ctx_qx<NX>(C, qx);
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYGT);
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* boost = C.at(C.L->boost);
   const gdouble* dh = C.at(C.L->dh);
@@ -392,7 +392,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
 template <class X, int NX, int NU>
 BMPC_HD void apply_A(const X ex, const Ctx& C, const gdouble* zv, gdouble* out) {
   CPlan& P = *C.P;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const gdouble* Ad = C.at(C.L->Ad);
   const gdouble* Bd = C.at(C.L->Bd);
   struct V4 { double v[NX]; };
@@ -433,7 +433,7 @@ BMPC_HD void apply_A(const X ex, const Ctx& C, const gdouble* zv, gdouble* out) 
 template <class X, int NX, int NU>
 BMPC_HD void apply_AT(const X ex, const Ctx& C, const gdouble* y, gdouble* out) {
   CPlan& P = *C.P;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const gdouble* Ad = C.at(C.L->Ad);
   const gdouble* Bd = C.at(C.L->Bd);
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -492,7 +492,7 @@ BMPC_HD void apply_AT(const X ex, const Ctx& C, const gdouble* y, gdouble* out) 
 template <class X, int NX, int NU>
 BMPC_HD void build_hb(const X ex, const Ctx& C, gdouble* h, gdouble* bv) {
   CPlan& P = *C.P;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* h0 = C.at(C.L->h0);
   for (int it = ex.lane; it < P.T * Nc; it += ex.nlanes) {
@@ -848,7 +848,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin) {
   CPlan& P = *C.P;
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_FACTOR);
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const gdouble* dl = ws + L.dl;
@@ -1065,7 +1065,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_TREESOLVE);
   BMPC_COUNT(C.ws, L, PROF_NTREE);
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   gdouble* lv_ = ws + L.lvec;   // [nr][T][NX]

@@ -24,7 +24,8 @@ struct QpCtx {
 };
 
 // u node whose input created x node k's state (the rate-cost predecessor of x_u[k]); -1 root
-BMPC_HD int qp_pred_u(const TopoL& t, int u) { return t.x_srcu[t.u_x[u]]; }
+template <class T>
+BMPC_HD int qp_pred_u(const T& t, int u) { return t.x_srcu[t.u_x[u]]; }
 
 // coefficient j of inequality row c of state node k: Ncol collision rows (-dh) then the Fx rows
 template <int NX>
@@ -33,7 +34,8 @@ BMPC_HD double qp_row(CPlan& P, const gdouble* dh, int k, int c, int j) {
 }
 // rows of state node k are live: every node with an input, and robustMPC's terminal node
 // (its Fx rows carry slacks, MPC_branch.py:1470-1472); BranchMPC's leaf terminals are empty
-BMPC_HD bool qp_rows_on(CPlan& P, const TopoL& t, int k) { return t.x_u[k] >= 0 || P.desc.controller == BMPC_CTRL_ROBUST; }
+template <class T>
+BMPC_HD bool qp_rows_on(CPlan& P, const T& t, int k) { return t.x_u[k] >= 0 || P.desc.controller == BMPC_CTRL_ROBUST; }
 
 // ---- cost, rhs (buildCost / buildIneqConstr / buildEqConstr of the current tree) ----------
 template <class X, class M>
@@ -42,7 +44,7 @@ BMPC_FN void qp_build(const X ex, const QpCtx Cin, gdouble* hv, gdouble* bv) {
   constexpr int NX = M::NX, NU = M::NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   gdouble* ws = C.ws;
   const int Nc = P.Nc;
   const gdouble* w = ws + L.w;
@@ -155,7 +157,7 @@ BMPC_FN void qp_apply_P(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const gdouble* ws = C.ws;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
     const gdouble* H = ws + L.hx + k * NX * NX;
@@ -199,7 +201,7 @@ BMPC_FN void qp_apply_G(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.ws + L.dh;
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
@@ -225,7 +227,7 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble*
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.ws + L.dh;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -257,7 +259,7 @@ template <class X, int NX, int NU>
 BMPC_FN void qp_apply_E(const X ex, const QpCtx Cin, const gdouble* zv, gdouble* out) {
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const gdouble* Ad = C.ws + C.L->Ad;
   const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -278,7 +280,7 @@ template <class X, int NX, int NU>
 BMPC_FN void qp_apply_ET(const X ex, const QpCtx Cin, const gdouble* y, gdouble* out) {
   const QpCtx C = Cin.uniform();
   CPlan& P = *C.P;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const gdouble* Ad = C.ws + C.L->Ad;
   const gdouble* Bd = C.ws + C.L->Bd;
   for (int k = ex.lane; k < P.T; k += ex.nlanes) {
@@ -317,7 +319,7 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
   constexpr int NS = NX + NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const double qs2 = 2.0 * P.desc.Qslack[0];
@@ -456,7 +458,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
   constexpr int NS = NX + NU;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
-  const TopoL t = topo_view(P, ex);
+  const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   const gdouble* dh = ws + L.dh;

@@ -25,6 +25,7 @@ struct HostExecT {
   int lane = 0;
   int nlanes = 1;
   double* lds = nullptr;      // stands in for the wave's LDS scratch
+  using tab_ptr = const int32_t*;
   const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
   double* eco = nullptr;      // ... and for the per-ego constants (kTransform)
   static constexpr int kTaskLanes = 1;
