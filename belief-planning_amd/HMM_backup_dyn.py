@@ -15,7 +15,80 @@ from highway_branch_dyn import backup_brake, backup_maintain, dubin, lane_bdry_h
 from highway_branch_dyn import softmax, softmin, softsat  # noqa: F401
 
 __all__ = ["np", "PredictiveModel", "backup_trans", "veh_col", "dubin", "propagate_backup", "softsat",
-           "backup_maintain", "backup_brake"]
+           "backup_maintain", "backup_brake", "softmin", "softmax", "X_bdry", "veh_con", "dubin_fg", "dubin_f_x",
+           "generate_backup_traj", "backup_input_prob"]
+
+
+def softmin(x, y, gamma=1):
+    """Two-argument soft minimum of this module (:117-118; highway_branch_dyn's takes a vector)."""
+    return (np.exp(-gamma * x) * x + np.exp(-gamma * y) * y) / (np.exp(-gamma * x) + np.exp(-gamma * y))
+
+
+def softmax(x, y, gamma=1):
+    """Two-argument soft maximum (:120-121)."""
+    return (np.exp(gamma * x) * x + np.exp(gamma * y) * y) / (np.exp(gamma * x) + np.exp(gamma * y))
+
+
+def X_bdry(x, bdry, width):
+    """Distance to the nearer road edge and its gradient (:10-16)."""
+    dy1 = x[1] - bdry[0] - width / 2
+    dy2 = bdry[1] - x[1] - width / 2
+    return (dy1, np.array([0, 1, 0, 0])) if dy1 < dy2 else (dy2, np.array([0, -1, 0, 0]))
+
+
+def veh_con(x, x0, umax, ignore_x=True):
+    """LQR-like lane keeping toward x0, clipped to +-umax (:18-28)."""
+    if ignore_x:
+        u = np.array([-0.8558 * (x[2] - x0[2]), -0.3162 * (x[1] - x0[1]) - 3.9889 * (x[3] - x0[3])])
+    else:
+        u = np.array([-0.3162 * (x[0] - x0[0]) - 0.8558 * (x[2] - x0[2]),
+                      -0.3162 * (x[1] - x0[1]) - 3.9889 * (x[3] - x0[3])])
+    return np.minimum(umax, np.maximum(-umax, u))
+
+
+def dubin_fg(x):
+    """Control-affine split of the unicycle (:39-42): xdot = f(x) + g u."""
+    f = np.array([x[2] * np.cos(x[3]), x[2] * np.sin(x[3]), 0.0, 0.0])
+    g = np.array([[0, 0], [0, 0], [1, 0], [0, 1]], float)
+    return f, g
+
+
+def dubin_f_x(x, con, h=1e-6):
+    """Closed-loop Jacobian d(f(x, con(x)))/dx with central differences of con (:43-54)."""
+    dudx = np.zeros([4, 2])
+    for k in range(4):
+        e = np.zeros(4)
+        e[k] = h
+        dudx[k] = (con(x + e) - con(x - e)) / 2 / h
+    return np.concatenate((np.array([[0, 0, np.cos(x[3]), -x[2] * np.sin(x[3])],
+                                     [0, 0, np.sin(x[3]), x[2] * np.cos(x[3])]]), dudx.transpose()))
+
+
+def generate_backup_traj(x, con, stop_crit, f0, ts=0.05, sensitivity=True):
+    """Euler rollout of x under con until stop_crit(x, t) (:56-94), with the sensitivity
+    Q = dx_t/dx_0 and Qt = xdot - f0 per step when asked: (tt, xx, uu, QQ, Qt)."""
+    t, tt, xx, uu, QQ, Qt = 0, [], [], [], [], []
+    Q = np.identity(4)
+    while not stop_crit(x, t):
+        u = con(x)
+        xdot = np.array([x[2] * np.cos(x[3]), x[2] * np.sin(x[3]), u[0], u[1]])
+        if sensitivity:
+            QQ.append(Q)
+            ja = dubin_f_x(x, con)
+            Qt.append(xdot - f0)
+        tt.append(t)
+        xx.append(x)
+        uu.append(u)
+        x = x + xdot * ts
+        if sensitivity:
+            Q = Q + np.matmul(ja, Q) * ts
+        t = t + ts
+    return tt, xx, uu, QQ, Qt
+
+
+def backup_input_prob(cbfcond, cons):
+    """Likelihood of a backup given its CBF condition (:103-104)."""
+    return softsat(cbfcond - cons.c2, cons.s2)
 
 
 def backup_trans(h, cons):

@@ -23,16 +23,22 @@ def osqp_upper(P):
     return (U + sp.triu(U, 1).T).tocsc()
 
 
+INF = 1e20    # |bound| >= INF is infinite (OSQP_INFTY = 1e30)
+
+
 def osqp_like_solve(prob, tol=1e-10, maxit=100, verbose=False):
-    """min 1/2 x'Px + q'x  s.t. l <= Ax <= u with rows either l == u or l == -inf."""
+    """min 1/2 x'Px + q'x  s.t. l <= Ax <= u (OSQP's form): rows with l == u are equalities,
+    every other finite bound is a one-sided row (a'x <= u, -a'x <= -l), free rows drop."""
     P = osqp_upper(prob.P)
     q = prob.q
     A = sp.csr_matrix(prob.A)
-    l, u = prob.l, prob.u
-    eq = np.isfinite(l) & (l == u)
-    ineq = ~np.isfinite(l)
+    l, u = np.asarray(prob.l, float), np.asarray(prob.u, float)
+    fl, fu = l > -INF, u < INF
+    eq = fl & fu & (l == u)
+    up, lo = fu & ~eq, fl & ~eq
     E, e = A[eq].tocsc(), u[eq]
-    G, g = A[ineq].tocsc(), u[ineq]
+    G = sp.vstack([A[up], -A[lo]]).tocsc()
+    g = np.concatenate([u[up], -l[lo]])
     n, p, m = P.shape[0], E.shape[0], G.shape[0]
 
     def kkt(dsz):
@@ -55,16 +61,17 @@ def osqp_like_solve(prob, tol=1e-10, maxit=100, verbose=False):
     s = s + a + 1.0
     z = np.maximum(np.abs(z), 1.0)
     status = -2
-    nq = max(1.0, np.linalg.norm(q, np.inf))
+    ninf = lambda v: float(np.max(np.abs(v))) if len(v) else 0.0
+    nq = max(1.0, ninf(q))
     for it in range(maxit):
         rd = P @ x + q + E.T @ y + G.T @ z
         re = E @ x - e
         rg = G @ x + s - g
-        mu = s @ z / m
+        mu = s @ z / m if m else 0.0
         if verbose:
-            print(it, np.linalg.norm(rd, np.inf), np.linalg.norm(re, np.inf), np.linalg.norm(rg, np.inf), mu)
-        if (np.linalg.norm(rd, np.inf) < tol * nq and np.linalg.norm(re, np.inf) < tol * max(1, np.linalg.norm(e, np.inf))
-                and np.linalg.norm(rg, np.inf) < tol * max(1, np.linalg.norm(g, np.inf)) and mu < tol):
+            print(it, ninf(rd), ninf(re), ninf(rg), mu)
+        if (ninf(rd) < tol * nq and ninf(re) < tol * max(1, ninf(e))
+                and ninf(rg) < tol * max(1, ninf(g)) and mu < tol):
             status = 1
             break
         K, lu = kkt(s / z)
@@ -76,9 +83,9 @@ def osqp_like_solve(prob, tol=1e-10, maxit=100, verbose=False):
             return min(1.0, np.min(-v[neg] / dv[neg])) if np.any(neg) else 1.0
 
         aa = min(amax(s, ds), amax(z, dz))
-        mua = (s + aa * ds) @ (z + aa * dz) / m
-        sig = (mua / mu) ** 3
-        corr = (ds * dz - sig * mu) / z
+        mua = (s + aa * ds) @ (z + aa * dz) / m if m else 0.0
+        sig = (mua / mu) ** 3 if mu > 0 else 0.0
+        corr = (ds * dz - sig * mu) / z if m else np.zeros(0)
         dx, dy, dz = solve(K, lu, np.concatenate([-rd, -re, -rg + s + corr]))
         ds = -s - (s / z) * dz - corr
         a = 0.99 * min(amax(s, ds), amax(z, dz))

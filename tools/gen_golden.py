@@ -590,6 +590,66 @@ def gen_belief(name, M, m, N, z0, true_j, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+def gen_belief_env(name, M, m, N, T, seed, N_lane, out):
+    """Highway_env.sim's scene (Highway_env.py:48-382), the reference's own env driving the
+    reference's PredictiveControllers.MPC (:121 fixed as in gen_belief) over its HMM model,
+    the backup-CBF QPs of the other vehicles through the osqp stub (oracle QP, general
+    bounds), random and np.random seeded with ``seed`` before the env is built.  matplotlib
+    (plotting only) is stubbed when absent."""
+    from gen_golden_model import import_reference_models
+    _, _, HM, utils = import_reference_models()
+    import importlib
+    try:
+        importlib.import_module("matplotlib")
+    except ImportError:
+        for mod in ("matplotlib", "matplotlib.pyplot", "matplotlib.patches", "matplotlib.animation"):
+            sys.modules.setdefault(mod, types.ModuleType(mod))
+        sys.modules["matplotlib"].pyplot = sys.modules["matplotlib.pyplot"]
+        sys.modules["matplotlib"].patches = sys.modules["matplotlib.patches"]
+        sys.modules["matplotlib"].animation = sys.modules["matplotlib.animation"]
+    import random
+    import Highway_env as RHE
+    import Init_MPC
+    import PredictiveControllers as RPC
+    assert os.path.dirname(os.path.abspath(RHE.__file__)) == REF
+
+    class FixedMPC(RPC.MPC):
+        def get_xLin(self, x0, xbackup, b0):
+            if self.uLin is None:
+                self.uLin = np.zeros([self.N, self.d])
+            self.uLin = np.vstack((self.uLin, self.uLin[-1]))
+            self.xLin = np.zeros([self.N + 1, self.n])
+            xb = np.append(x0, np.reshape(b0, -1))
+            self.xLin[0] = xb
+            for i in range(0, self.N):
+                A, B, C, h0, Jh = self.predictiveModel.regressionAndLinearization(
+                    xb, xbackup[:, i * self.nx:(i + 1) * self.nx], self.uLin[i])
+                xbp = C + A.dot(xb) + B.dot(self.uLin[i])
+                self.xLin[i + 1] = xbp
+                xb = xbp
+
+    cons = utils.Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=6.0, rm=0.3, J_c=20, s_c=1,
+                                  ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    pols = [lambda x: HM.backup_maintain(x, cons), lambda x: HM.backup_brake(x, cons),
+            lambda x: np.array([-2.0, -cons.Kpsi * x[3]])][:m]
+    dt = 0.1
+    model = HM.PredictiveModel(4, 2, M, pols, dt, cons)
+    param = Init_MPC.initMPCParams(4, 2, N, M, m, 1.8, RHE.v0, cons.am, cons.rm, N_lane, cons.W)
+    mpc = FixedMPC(param, model)
+    random.seed(seed)
+    np.random.seed(seed)
+    env = RHE.Highway_env(NV=M + 1, mpc=mpc, N_lane=N_lane)
+    init = np.array([v.state for v in env.veh_set])
+    lanes0 = np.array([v.laneidx for v in env.veh_set])
+    state_rec, input_rec, backup_rec, choice_rec, b_rec, xPred_rec, collision = RHE.Highway_sim(env, T)
+    d_out = dict(M=M, m=m, N=N, dt=dt, T=T, seed=seed, N_lane=N_lane, am=cons.am, rm=cons.rm, W=cons.W,
+                 init=init, lanes0=lanes0, state_rec=state_rec, input_rec=input_rec,
+                 choice_rec=np.array(choice_rec, float), b_rec=np.array(b_rec), xPred_rec=np.array(xPred_rec),
+                 collision=int(collision))
+    print(f"[{name}] {state_rec.shape[1]} steps, collision={collision}, final states {state_rec[:, -1]}")
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -609,6 +669,7 @@ def main():
         "highway_robust_n8_nb2": lambda: gen_highway_robust("highway_robust_n8_nb2", 8, 2, 5 if a.quick else 20, {0, 1, 10}, out),
         "quadruped_n25_nb2": lambda: gen_quadruped("quadruped_n25_nb2", 3 if a.quick else 40, {0, 1, 2, 20}, out),
         "merge_n40_nb1": lambda: gen_merge("merge_n40_nb1", 4 if a.quick else 60, {0, 1, 2, 30, 45}, out),
+        "belief_env_m2": lambda: gen_belief_env("belief_env_m2", 2, 3, 10, 3.0, 7, 3, out),
         "belief_m1": lambda: gen_belief("belief_m1", 1, 3, 10, [[10.0, 1.8, 12.0, 0.0]], [1], 12, {0, 1, 6}, out),
         "belief_m2": lambda: gen_belief("belief_m2", 2, 2, 8, [[12.0, 1.8, 12.0, 0.0], [-6.0, 5.4, 17.0, 0.0]], [1, 0],
                                         10, {0, 4}, out),
