@@ -123,6 +123,7 @@ struct Plan {
   int nsm;    // dense coupling system size
   // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
   int lds_M, lds_piv, lds_rhs, lds_red, nlds;
+  int nlds_lean;            // LDS doubles when the coupling system lives in the slab (Layout::coup)
   int lds_scr, nscr;       // tree-solve LDS scratch (slack terms of the pre-pass; 0 = none)
   int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
   double W1[BMPC_MAX_N * BMPC_MAX_N];   // sqrtm(Q) / chol(Q)'  (MPC_branch.py:1628-1631)
@@ -183,6 +184,7 @@ struct Layout {
   size_t dl, dli, eta, wbar, vnt;   // NT scaling: LP d and 1/d, cone eta, wbar, v
   // KKT
   size_t hx, hu, sd, P, Kg, Luu, kff, lvec, qx0, gk, colk, colnu;
+  size_t coup;    // coupling matrix | pivots | rhs when they are not in LDS (lean-LDS launches)
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
   // BranchMPCProx QP: u-rate couplings, linear cost, augmented Riccati P~, [Kx Kv], l~
   size_t qo, qq, Pa, Ka, la;

@@ -40,7 +40,9 @@ __device__ __forceinline__ double dpp_d(double v) {
 template <bool TR, bool TL = true>
 struct DevExecT {
   static constexpr bool kTransform = TR;   // per-ego S / bx constants in LDS (merge plans)
-  // topology tables: the wave's LDS copy (TL) or the plan's blob in global memory
+  // LDS-rich launch (TL): topology tables copied to LDS and the coupling system in LDS;
+  // lean launch: tables read from the plan's blob, coupling system in the slab
+  static constexpr bool kCoupLds = TL;
   using tab_ptr = typename std::conditional<TL, lint*, gint*>::type;
   int lane;
   ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm / k_qp only)
@@ -104,9 +106,9 @@ struct Bundle {
 // topology tables (Plan::ntab int32), then (transform-capable models) ECO_COUNT doubles of
 // per-ego constants.  The table copy is one batched pass at kernel start; every later tree /
 // cone / node-index lookup of the solve is an LDS read.
-__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform, bool topo_lds) {
-  const size_t tab = topo_lds ? (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7 : 0;
-  return sizeof(double) * (size_t)P.nlds + tab + (transform ? sizeof(double) * ECO_COUNT : 0);
+__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform, bool rich) {
+  const size_t tab = rich ? (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7 : 0;
+  return sizeof(double) * (size_t)(rich ? P.nlds : P.nlds_lean) + tab + (transform ? sizeof(double) * ECO_COUNT : 0);
 }
 template <bool TR, bool TL>
 __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* lds_dyn) {
@@ -122,11 +124,12 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
   }
 }
 
-// LDS copy of the topology tables only when it costs no resident wave: a workgroup's LDS
-// bounds the egos per CU (160 KB / bytes, at most 16 with 4 waves per SIMD), and deep trees
-// (N=30, NB=2: 17 KB of tables) would lose 3 of 7.  BMPC_TOPO_LDS=0/1 forces either.
-static bool choose_topo_lds(const Plan& P, bool transform) {
-  if (const char* e = getenv("BMPC_TOPO_LDS")) return atoi(e) != 0;
+// LDS-rich launch (topology tables and coupling system in LDS) only when it costs no
+// resident ego: a workgroup's LDS bounds the egos per CU (160 KB / bytes, at most 16 with 4
+// waves per SIMD).  Deep trees (N=30, NB=2: 17 KB of tables, a 20 KB coupling matrix) run
+// lean, 16 egos per CU instead of 4.  BMPC_LDS_RICH=0/1 forces either.
+static bool choose_lds_rich(const Plan& P, bool transform) {
+  if (const char* e = getenv("BMPC_LDS_RICH")) return atoi(e) != 0;
   auto egos = [](size_t b) { return std::min<size_t>(16, (160 * 1024) / std::max<size_t>(b, 1)); };
   return egos(solver_lds_bytes(P, transform, true)) >= egos(solver_lds_bytes(P, transform, false));
 }
@@ -519,7 +522,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
   const bool merge = P.desc.model == BMPC_MODEL_HIGHWAY_MERGE;
-  const bool tl = choose_topo_lds(P, merge);
+  const bool tl = choose_lds_rich(P, merge);
   size_t lds_bytes = solver_lds_bytes(P, merge, tl);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)

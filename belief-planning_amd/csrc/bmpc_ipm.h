@@ -1327,8 +1327,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 }
 
 // dense LU with partial pivoting of the coupling system (row-major n x n, in LDS)
-template <class X>
-BMPC_FN bool small_lu(const X ex, ldouble* M, ldouble* piv, int n) {
+template <class X, class PM, class PP>
+BMPC_FN bool small_lu(const X ex, PM* M, PP* piv, int n) {
   for (int k = 0; k < n; ++k) {
     double best = -1.0, bi = 1e300;
     for (int i = k + ex.lane; i < n; i += ex.nlanes) {
@@ -1359,8 +1359,8 @@ BMPC_FN bool small_lu(const X ex, ldouble* M, ldouble* piv, int n) {
 }
 
 // solve with the LU above; b in LDS, column-oriented substitution (one step per row)
-template <class X>
-BMPC_HD void small_lu_solve(const X ex, const ldouble* M, const ldouble* piv, ldouble* b, int n) {
+template <class X, class PM, class PB>
+BMPC_HD void small_lu_solve(const X ex, const PM* M, const PM* piv, PB* b, int n) {
   if (ex.lane == 0)
     for (int k = 0; k < n; ++k) {
       const int p = (int)piv[k];
@@ -1385,6 +1385,14 @@ BMPC_HD void small_lu_solve(const X ex, const ldouble* M, const ldouble* piv, ld
   }
 }
 
+// the dense coupling system (matrix | pivots | rhs at the plan's lds_M / lds_piv / lds_rhs):
+// in LDS, or in the ego's slab for lean-LDS launches (X::kCoupLds false)
+template <class X>
+BMPC_HD auto coup_mem(const X& ex, gdouble* ws, CLayout& L, CPlan& P, int off) {
+  if constexpr (X::kCoupLds) return ex.lds + off;
+  else return ws + L.coup + (off - P.lds_M);
+}
+
 // global variable index -> position in the primal vector
 BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
 
@@ -1399,7 +1407,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
   const int nc = P.ncones;
   tree_solve<X, NX, NU>(ex, C, nc, ws + L.gk, P.nv, ws + L.zeros, 0, ws + L.colk, P.nv, ws + L.colnu, P.neq);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
-  ldouble* M = ex.lds + P.lds_M;
+  auto* M = coup_mem(ex, ws, L, P, P.lds_M);
   const gdouble* eta = ws + L.eta;
   const gdouble* dl = ws + L.dl;
   const gdouble* p = ws + L.p;
@@ -1457,7 +1465,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
     M[(ng + nb + k) * ns + i] = -ck * gv;
   }
   ex.sync();
-  return small_lu(ex, M, ex.lds + P.lds_piv, ns);
+  return small_lu(ex, M, coup_mem(ex, ws, L, P, P.lds_piv), ns);
 }
 
 // One pass of the W-scaled KKT system (oracle/ecos_ipm.py KKT)
@@ -1476,7 +1484,7 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   apply_GT<X, NX, NU>(ex, C, tr, tz, r1);         // G' W^-1 r3h + r1
   tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
-  ldouble* b = ex.lds + P.lds_rhs;
+  auto* b = coup_mem(ex, ws, L, P, P.lds_rhs);
   const gdouble* eta = ws + L.eta;
   for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
     const int na = nc - k0 < 4 ? nc - k0 : 4;
@@ -1487,8 +1495,8 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   }
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
-  small_lu_solve(ex, ex.lds + P.lds_M, ex.lds + P.lds_piv, b, ns);
-  const ldouble* bc = b + ng + nb;
+  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_mem(ex, ws, L, P, P.lds_piv), b, ns);
+  const auto* bc = b + ng + nb;
   const gdouble* colk = ws + L.colk;
   const gdouble* colnu = ws + L.colnu;
   // dx (tree and slack parts) and dy in one pass; the columns are loaded four at a time so a

@@ -247,11 +247,6 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.nlp = P.rPos + T * P.Nc;
   P.ng = bd * (2 * m + 2) + 1;
   P.nsm = P.ng + bd + P.ncones;
-  P.lds_M = 0;
-  P.lds_piv = P.nsm * P.nsm;
-  P.lds_rhs = P.lds_piv + P.nsm;
-  P.lds_red = P.lds_rhs + P.nsm;
-  P.nlds = P.lds_red + 64;
   P.cgrp = 64;
   while (P.cgrp > 1 && P.cgrp * P.ncones > 64) P.cgrp >>= 1;
 
@@ -300,14 +295,22 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
     P.nrows = P.nlp;
     P.ng = 0;
     P.nsm = 0;
-    P.lds_M = P.lds_piv = P.lds_rhs = P.lds_red = 0;
-    P.nlds = 64;
   }
-  // tree-solve scratch (CVaR IPM): the pre-pass slack terms, T * Nc doubles, while the
-  // per-workgroup LDS stays within 9,984 bytes (16 egos per CU)
-  P.lds_scr = P.nlds;
-  P.nscr = desc.controller == BMPC_CTRL_CVAR && P.nlds + T * P.Nc <= 1248 ? T * P.Nc : 0;
-  P.nlds += P.nscr;
+  // LDS of the solver kernels (doubles): a 64-double reduction area, the tree-solve scratch
+  // (CVaR IPM: the pre-pass slack terms, T * Nc doubles, while the whole stays within 9,984
+  // bytes = 16 egos per CU), then the dense coupling system (matrix, pivots, rhs).  A lean-LDS
+  // launch (bmpc_hip.hip, choose_lds_rich) keeps only the part before the coupling system and
+  // finds the system in the slab (Layout::coup) -- deep trees, whose 50 x 50 system would
+  // otherwise leave 7 egos per CU.
+  const int ncoup = P.nsm * P.nsm + 2 * P.nsm;
+  P.lds_red = 0;
+  P.lds_scr = 64;
+  P.nscr = desc.controller == BMPC_CTRL_CVAR && 64 + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
+  P.lds_M = P.lds_scr + P.nscr;
+  P.lds_piv = P.lds_M + P.nsm * P.nsm;
+  P.lds_rhs = P.lds_piv + P.nsm;
+  P.nlds = P.lds_rhs + P.nsm;
+  P.nlds_lean = P.lds_M;
 
   // ---- weights -----------------------------------------------------------------------------
   double Qm[BMPC_MAX_N * BMPC_MAX_N], Rm[BMPC_MAX_D * BMPC_MAX_D];
@@ -420,6 +423,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.colk = take((size_t)nc * nv);
   L.colnu = take((size_t)nc * neq);
   L.prof = take(PROF_COUNT);
+  L.coup = take((size_t)P.nsm * P.nsm + 2 * (size_t)P.nsm);
   if (desc.controller != BMPC_CTRL_CVAR) {   // QP-only arrays (augmented-state Riccati)
     const int NS = n + d;
     L.qo = take((size_t)U * d * d);

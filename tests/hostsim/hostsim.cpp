@@ -19,9 +19,10 @@
 using namespace bmpc;
 
 namespace {
-template <bool TR>
+template <bool TR, bool CL = true>
 struct HostExecT {
   static constexpr bool kTransform = TR;
+  static constexpr bool kCoupLds = CL;   // coupling system in the LDS stand-in (else the slab, as lean launches)
   int lane = 0;
   int nlanes = 1;
   double* lds = nullptr;      // stands in for the wave's LDS scratch
@@ -108,15 +109,20 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   {
   HostExec ex;
   HostExecT<true> exm;
+  HostExecT<false, false> exl;          // BMPC_HOST_LEAN=1: the lean-LDS launch's slab coupling system
+  const char* lean_env = getenv("BMPC_HOST_LEAN");
+  const bool lean = lean_env && atoi(lean_env) != 0;
   std::vector<double> lds(P.nlds), eco(ECO_COUNT);
-  ex.lds = exm.lds = lds.data();
-  ex.tab = exm.tab = P.t.br_depth;      // the host blob (first table at offset 0)
+  ex.lds = exm.lds = exl.lds = lds.data();
+  ex.tab = exm.tab = exl.tab = P.t.br_depth;      // the host blob (first table at offset 0)
   exm.eco = eco.data();
 #pragma omp for schedule(dynamic, 4)
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;
-    if (P.desc.model == BMPC_MODEL_HIGHWAY)
+    if (P.desc.model == BMPC_MODEL_HIGHWAY && lean)
+      r = solve_ego<HostExecT<false, false>, Highway>(exl, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY)
       r = solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
     else if (P.desc.model == BMPC_MODEL_HIGHWAY_MERGE)
       r = solve_ego<HostExecT<true>, HighwayMerge>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);

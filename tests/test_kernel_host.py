@@ -75,3 +75,22 @@ def test_host_build_seeded_batch_statuses():
         u0 = r["upred"][:, 0]
         x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
         z = z + 0.1 * np.stack([z[:, 2] * np.cos(z[:, 3]), z[:, 2] * np.sin(z[:, 3]), 0 * z[:, 0], 0 * z[:, 0]], 1)
+
+
+def test_lean_lds_path_matches(monkeypatch):
+    """The lean-LDS launch keeps the dense coupling system in the ego's slab (Layout::coup)
+    instead of LDS (deep trees: 16 egos per CU instead of 4).  The host build of that path
+    (BMPC_HOST_LEAN=1) gives the same replay of the N=8, NB=2 loop (50 x 50 coupling system)
+    as the LDS path, bit for bit."""
+    g = golden("highway_n8_nb2")
+    rb = replay_batch(g, 12)
+    out = []
+    for lean in ("0", "1"):
+        monkeypatch.setenv("BMPC_HOST_LEAN", lean)
+        hs = H.HostSim(highway_desc_from_golden(g), rb["T"])
+        hs.set_policies(rb["rows"])
+        hs.set_warm_start(rb["uLin"], rb["p"], rb["jcons"])
+        hs.reset_mask(~rb["warm"])
+        out.append(hs.solve(rb["x"], rb["z"], rb["xref"]))
+    for k in ("status", "iters", "J", "upred"):
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
