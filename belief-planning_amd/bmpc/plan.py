@@ -210,9 +210,10 @@ def qp_arrays(P, q, A, l, u):
     325).  A batch's pattern is the union of its members' patterns."""
     import scipy.sparse as sp
     many = isinstance(P, (list, tuple))
-    Ps = [sp.triu(sp.csc_matrix(p), format="csc") for p in (P if many else [P])]
-    As = [sp.csc_matrix(a) for a in (A if many else [A])]
-    B = len(Ps)
+    B = len(P) if many else 1
+    same = many and all(p is P[0] for p in P) and all(a is A[0] for a in A)   # one matrix pair, B right sides
+    Ps = [sp.triu(sp.csc_matrix(p), format="csc") for p in ([P[0]] if same else P if many else [P])]
+    As = [sp.csc_matrix(a) for a in ([A[0]] if same else A if many else [A])]
     n = Ps[0].shape[1]
     m = As[0].shape[0]
 
@@ -229,7 +230,9 @@ def qp_arrays(P, q, A, l, u):
         return pat.indptr.astype(np.int32), pat.indices.astype(np.int32), vals
 
     Pp, Pi, Px = pattern(Ps)
-    Ap, Ai, Ax = pattern(As) if m else (np.zeros(n + 1, np.int32), np.zeros(0, np.int32), np.zeros((B, 0)))
+    Ap, Ai, Ax = pattern(As) if m else (np.zeros(n + 1, np.int32), np.zeros(0, np.int32), np.zeros((len(As), 0)))
+    if same:
+        Px, Ax = np.repeat(Px, B, axis=0), np.repeat(Ax, B, axis=0)
     def f2(a, k):
         a = np.asarray(a, np.float64)
         return np.ascontiguousarray(np.broadcast_to(a.reshape(-1, k) if k else np.zeros((B, 0)), (B, k)))

@@ -7,7 +7,7 @@
 // ADMM is not restated: like the oracle (oracle/qp_ipm.py) the kernel returns the QP optimum
 // by a Mehrotra predictor-corrector interior-point method.
 //
-// Rows are split by the host (bmpc_bandqp.cpp) into equalities (l == u) and one-sided
+// Rows are split by the host (bmpc_qpplan.cpp) into equalities (l == u) and one-sided
 // inequality copies (a'x <= u, -a'x <= -l).  Each Newton step solves the quasidefinite KKT
 // system
 //
@@ -21,8 +21,9 @@
 //
 // Execution: one 64-lane wave per problem.  The factorisation streams the band through a
 // (bw+1) x (bw+1) ring window in LDS -- each rank-1 update touches only rows k+1..k+bw, so
-// every band entry is read from HBM once and written once per factorisation; the solve
-// vector lives in LDS too.  Everything else is O(nk*bw) per iteration.  Vectors are kept in
+// every band entry is read from HBM once per factorisation; the factor itself stays in LDS
+// when it fits beside the window (nk*(bw+1) doubles: 100 KB for the belief MPC's 400 x 32
+// band), so the triangular sweeps of the solves read LDS; the solve vector lives in LDS too.  Everything else is O(nk*bw) per iteration.  Vectors are kept in
 // "KKT space" (the permuted index of the x, y and z blocks) so every IPM vector operation
 // is one strided loop.
 //
@@ -48,6 +49,7 @@ struct BandQPDesc {
   int32_t nvals, ncvals; // values per problem: [Px; Ax] and [q; l; u]
   int32_t nscat, ncscat; // entries of the two scatter lists
   int32_t max_iter;
+  int32_t lb_lds;        // the factor L D L' lives in LDS (it fits beside the window), else in the workspace
   double eps;            // convergence tolerance (oracle/qp_ipm.py's tol)
   const int32_t* kind;   // [nk] QPK_* of each KKT row
   const int32_t* scat;   // [nscat][3]: src in [Px; Ax], band index dst, sign
@@ -63,8 +65,12 @@ struct BandQPWs {
 };
 
 BMPC_HD size_t bandqp_stride(int nk, int W) { return 2 * (size_t)nk * W + 11 * (size_t)nk; }
-// LDS: the factorisation window (W*W), its column of multipliers (W), the solve vector (nk)
-BMPC_HD size_t bandqp_lds_doubles(int nk, int W) { return (size_t)W * W + W + nk; }
+// LDS: the factorisation window (W*W), its column of multipliers (W), the solve vector (nk),
+// then (lb_lds) the factor itself (nk*W): the eight triangular sweeps of an iteration then
+// read LDS instead of global memory
+BMPC_HD size_t bandqp_lds_doubles(int nk, int W, bool lb_lds) {
+  return (size_t)W * W + W + nk + (lb_lds ? (size_t)nk * W : 0);
+}
 
 BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
   BandQPWs v;
@@ -101,8 +107,8 @@ BMPC_HD void bqp_matvec(const X& ex, const BandQPDesc& d, const double* Kb, cons
 // L[i][i-k] for k = 1..bw and D[i] at k = 0.  Right-looking, rows k..k+bw of the active
 // submatrix resident in the LDS ring window.  A pivot of the wrong sign or below 1e-13 in
 // magnitude is replaced by +-2e-7 (ECOS's dynamic regularisation constants).
-template <class X>
-BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, double* Lb) {
+template <class X, class LP>
+BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* Lb) {
   const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
   auto* win = ex.lds;
   auto* lv = ex.lds + (size_t)W * W;
@@ -143,8 +149,8 @@ BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, cons
 }
 
 // out = (L D L')^{-1} b; column sweeps on the LDS solve vector
-template <class X>
-BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const double* Lb, const double* b, double* out) {
+template <class X, class LP>
+BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const LP* Lb, const double* b, double* out) {
   const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
   auto* y = ex.lds + (size_t)W * W + W;
   for (int i = ex.lane; i < nk; i += nl) y[i] = b[i];
@@ -169,9 +175,10 @@ BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const double* Lb, c
 
 // out = K^{-1} b for the true matrix (Kb, diagonal tdg) through its regularised factor:
 // up to three refinement steps, stopping at a 1e-15 relative residual (oracle/qp_ipm.py).
-template <class X>
-BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs& v, const double* b, double* out) {
-  bqp_ldl_solve(ex, d, v.Lb, b, out);
+template <class X, class LP>
+BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs& v, const LP* Lb, const double* b,
+                               double* out) {
+  bqp_ldl_solve(ex, d, Lb, b, out);
   double bn = 0.0;
   for (int i = ex.lane; i < d.nk; i += ex.nlanes) bn = fmax(bn, fabs(b[i]));
   bn = ex.max(bn);
@@ -185,7 +192,7 @@ BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs&
     rn = ex.max(rn);
     ex.sync();
     if (rn < 1e-15 * fmax(1.0, bn)) break;
-    bqp_ldl_solve(ex, d, v.Lb, v.t1, v.t2);
+    bqp_ldl_solve(ex, d, Lb, v.t1, v.t2);
     for (int i = ex.lane; i < d.nk; i += ex.nlanes) out[i] += v.t2[i];
     ex.sync();
   }
@@ -203,11 +210,9 @@ BMPC_HD double bqp_step(const X& ex, const BandQPDesc& d, const BandQPWs& v) {
   return ex.min(a);
 }
 
-// One problem.  vals = [Px; Ax], cvals = [q; l; u] (the CSC value arrays of the shared
-// pattern); x [n], y [m] (OSQP's dual: P x + q + A'y = 0); returns the QP_* status.
-template <class X>
-BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
-                         double* x, double* y, int* iters) {
+template <class X, class LP>
+BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
+                           LP* Lb, double* x, double* y, int* iters) {
   const int nk = d.nk, nl = ex.nlanes, lane = ex.lane;
   const BandQPWs v = bandqp_ws(d, ws);
   const double rs = 1e-8;   // static regularisation (ECOS's STATIC_REG)
@@ -237,8 +242,8 @@ BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, c
     v.rhs[i] = kd == QPK_X ? -v.c[i] : v.c[i];
   }
   ex.sync();
-  bqp_factor(ex, d, v.Kb, v.fdg, v.Lb);
-  bqp_solve_refined(ex, d, v, v.rhs, v.w);
+  bqp_factor(ex, d, v.Kb, v.fdg, Lb);
+  bqp_solve_refined(ex, d, v, Lb, v.rhs, v.w);
   for (int i = lane; i < nk; i += nl) {
     v.t2[i] = d.kind[i] == QPK_X ? v.w[i] : 0.0;
     v.fdg[i] = d.kind[i] == QPK_X ? v.Kb[(size_t)i * d.W] : 0.0;   // diagonal of [P E' G'; E 0 0; G 0 0]
@@ -306,9 +311,9 @@ BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, c
       v.rhs[i] = kd == QPK_IN ? -v.r[i] + v.s[i] : -v.r[i];
     }
     ex.sync();
-    bqp_factor(ex, d, v.Kb, v.fdg, v.Lb);
+    bqp_factor(ex, d, v.Kb, v.fdg, Lb);
     // ---- predictor (affine) step
-    bqp_solve_refined(ex, d, v, v.rhs, v.dw);
+    bqp_solve_refined(ex, d, v, Lb, v.rhs, v.dw);
     for (int i = lane; i < nk; i += nl)
       v.ds[i] = d.kind[i] == QPK_IN ? -v.s[i] - v.s[i] / v.w[i] * v.dw[i] : 0.0;
     ex.sync();
@@ -329,7 +334,7 @@ BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, c
     // t2 is the refinement scratch: stash corr in ds first
     for (int i = lane; i < nk; i += nl) v.ds[i] = d.kind[i] == QPK_IN ? v.t2[i] : 0.0;
     ex.sync();
-    bqp_solve_refined(ex, d, v, v.rhs, v.dw);
+    bqp_solve_refined(ex, d, v, Lb, v.rhs, v.dw);
     for (int i = lane; i < nk; i += nl)
       if (d.kind[i] == QPK_IN) v.ds[i] = -v.s[i] - v.s[i] / v.w[i] * v.dw[i] - v.ds[i];
     ex.sync();
@@ -351,6 +356,15 @@ BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, c
   if (iters && lane == 0) *iters = it;
   ex.sync();
   return status;
+}
+
+// One problem.  vals = [Px; Ax], cvals = [q; l; u] (the CSC value arrays of the shared
+// pattern); x [n], y [m] (OSQP's dual: P x + q + A'y = 0); returns the QP_* status.
+template <class X>
+BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
+                         double* x, double* y, int* iters) {
+  if (d.lb_lds) return bandqp_solve_t(ex, d, vals, cvals, ws, ex.lds + (size_t)d.W * d.W + d.W + d.nk, x, y, iters);
+  return bandqp_solve_t(ex, d, vals, cvals, ws, bandqp_ws(d, ws).Lb, x, y, iters);
 }
 
 }  // namespace bmpc

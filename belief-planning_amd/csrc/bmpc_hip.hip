@@ -127,11 +127,14 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
 // LDS-rich launch (topology tables and coupling system in LDS) only when it costs no
 // resident ego: a workgroup's LDS bounds the egos per CU (160 KB / bytes, at most 16 with 4
 // waves per SIMD).  Deep trees (N=30, NB=2: 17 KB of tables, a 20 KB coupling matrix) run
-// lean, 16 egos per CU instead of 4.  BMPC_LDS_RICH=0/1 forces either.
-static bool choose_lds_rich(const Plan& P, bool transform) {
+// lean, 16 egos per CU instead of 4, unless the batch is resident either way.  BMPC_LDS_RICH=0/1
+// forces either.
+static bool choose_lds_rich(const Plan& P, bool transform, int batch) {
   if (const char* e = getenv("BMPC_LDS_RICH")) return atoi(e) != 0;
   auto egos = [](size_t b) { return std::min<size_t>(16, (160 * 1024) / std::max<size_t>(b, 1)); };
-  return egos(solver_lds_bytes(P, transform, true)) >= egos(solver_lds_bytes(P, transform, false));
+  const size_t rich = egos(solver_lds_bytes(P, transform, true));
+  // a batch that is resident either way (256 CUs) runs rich: residency is not what limits it
+  return (size_t)batch <= 256 * rich || rich >= egos(solver_lds_bytes(P, transform, false));
 }
 
 template <class M>
@@ -522,7 +525,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
   const bool merge = P.desc.model == BMPC_MODEL_HIGHWAY_MERGE;
-  const bool tl = choose_lds_rich(P, merge);
+  const bool tl = choose_lds_rich(P, merge, B);
   size_t lds_bytes = solver_lds_bytes(P, merge, tl);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
@@ -928,7 +931,7 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
   d.cscat = d.scat + h.scat.size();
   d.xmap = d.cscat + h.cscat.size();
   d.ymap = d.xmap + h.xmap.size();
-  const size_t lds = bandqp_lds_doubles(d.nk, d.W) * sizeof(double);
+  const size_t lds = bandqp_lds_doubles(d.nk, d.W, d.lb_lds) * sizeof(double);
   if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute((const void*)k_bandqp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k_bandqp, dim3(batch), dim3(64), lds, 0, d, dvals.as<double>(), dcvals.as<double>(),
                      dws.as<double>(), dx, dy, dst, dit, batch);

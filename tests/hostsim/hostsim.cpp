@@ -294,7 +294,7 @@ int hs_qp_solve(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_
     info[3] = h.d.nscat;
   }
   const int nnzP = Pp[n], nnzA = Ap[n];
-  std::vector<double> vals(h.d.nvals + 1), cvals(h.d.ncvals), ws(h.d.stride), lds(bandqp_lds_doubles(h.d.nk, h.d.W));
+  std::vector<double> vals(h.d.nvals + 1), cvals(h.d.ncvals), ws(h.d.stride), lds(bandqp_lds_doubles(h.d.nk, h.d.W, h.d.lb_lds));
   std::vector<double> ybuf(m + 1);
   HostExec ex;
   ex.lds = lds.data();
