@@ -298,7 +298,11 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
       status = QP_NUMERICS;
       break;
     }
-    if (rd < d.eps * nq && re < d.eps * ne && rg < d.eps * ng && mu < d.eps) {
+    double sn = 0.0;   // |s|: the inequality residual's scale, as in oracle/qp_ipm.py
+    for (int i = lane; i < nk; i += nl)
+      if (d.kind[i] == QPK_IN) sn = fmax(sn, fabs(v.s[i]));
+    sn = ex.max(sn);
+    if (rd < d.eps * nq && re < d.eps * ne && rg < d.eps * fmax(ng, sn) && mu < d.eps) {
       status = QP_SOLVED;
       break;
     }

@@ -736,7 +736,11 @@ BMPC_FN IpmResult qp_ipm(const X ex, const QpCtx Cin) {
 #ifdef BMPC_HOST_DEBUG
     printf("qp it %d rd %.3e re %.3e rg %.3e mu %.3e\n", it, amax_inf(nv, rd), amax_inf(neq, re), amax_inf(m, rg), mu);
 #endif
-    if (amax_inf(nv, rd) < tol * nq && amax_inf(neq, re) < tol * ne && amax_inf(m, rg) < tol * ng && mu < tol) {
+    // the inequality residual is judged against max(|g|, |s|) (OSQP's rule scales by the
+    // larger of |Ax| and |z|): G x + s - g cancels to the rounding floor of s, which is not
+    // bounded by |g| (quadruped config 4 stalled at rg = 9.3e-10 with |g| < 9)
+    const double ngs = fmax(ng, amax_inf(m, s));
+    if (amax_inf(nv, rd) < tol * nq && amax_inf(neq, re) < tol * ne && amax_inf(m, rg) < tol * ngs && mu < tol) {
       res.exit_flag = 1;
       break;
     }

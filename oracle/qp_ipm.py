@@ -70,8 +70,10 @@ def osqp_like_solve(prob, tol=1e-10, maxit=100, verbose=False):
         mu = s @ z / m if m else 0.0
         if verbose:
             print(it, ninf(rd), ninf(re), ninf(rg), mu)
+        # rg against max(|g|, |s|): OSQP scales the primal residual by max(|Ax|, |z|), and
+        # G x + s - g cancels to the rounding floor of s, which |g| does not bound
         if (ninf(rd) < tol * nq and ninf(re) < tol * max(1, ninf(e))
-                and ninf(rg) < tol * max(1, ninf(g)) and mu < tol):
+                and ninf(rg) < tol * max(1, ninf(g), ninf(s)) and mu < tol):
             status = 1
             break
         K, lu = kkt(s / z)

@@ -82,3 +82,23 @@ def test_robust_mpc_replay(name):
     np.testing.assert_array_equal(r["status"], g["traj_status"])
     np.testing.assert_allclose(r["upred"], g["traj_uPred"], atol=1e-6)
     np.testing.assert_allclose(r["xpred"], g["traj_xPred"], atol=1e-6)
+
+
+def test_quadruped_closed_loop_precision_floor():
+    """BASELINE config 4, seeded ego 311 of 1024: at step 7 the inequality residual
+    G x + s - g stalls at the rounding floor of s (9.3e-10) while |g| < 9, so a test scaled by
+    |g| alone never passed and the factorisation broke down at mu ~ 1e-17 (status -2).  Judged
+    against max(|g|, |s|) (OSQP scales by max(|Ax|, |z|)) every step solves
+    (tools/quad_failures.py: 0 of 20,480 closed-loop solves fail, host build and GPU)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from quad_failures import env_step
+    from bmpc.scenarios import quadruped_desc, seeded_quadruped_batch
+    x, z, xr = (v[311:312] for v in seeded_quadruped_batch(1024, seed=1))
+    hs = H.HostSim(quadruped_desc(), 1)
+    hs.set_policies(quadruped_policy_rows(1))
+    for t in range(8):
+        r = hs.solve(x, z, xr)
+        assert r["status"][0] == 1, (t, r["status"], r["iters"])
+        x, z, xr = env_step(x, z, r["upred"][:, 0])
