@@ -16,6 +16,12 @@
 
 #include "bmpc_tree.h"
 
+#ifndef BMPC_TS_UN
+#define BMPC_TS_UN 2         // elements per lane batch in the tree solve's slack pre- / post-passes (2: -1.1% k_ipm vs 4, 8: +15%)
+#endif
+#ifndef BMPC_TS_UN_AV
+#define BMPC_TS_UN_AV 8      // ... and in the pre-pass's slack-term pass
+#endif
 #ifndef BMPC_NITREF
 #define BMPC_NITREF 1        // refinement rounds per KKT solve (oracle: 3; 1 keeps parity)
 #endif
@@ -1087,13 +1093,13 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     const gdouble* rr = r0 + ri * rs;
     gdouble* q0 = q0_ + ri * lstr;
     if (av_lds) {
-      lane_batch<8>(ex, 0, P.T * Nc, [&](int it) {
+      lane_batch<BMPC_TS_UN_AV>(ex, 0, P.T * Nc, [&](int it) {
         const int k = it / Nc;
         const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // terminal nodes add 0
         return on * sdv[it * 2 + 1] * rr[P.oS + it] / sdv[it * 2];
       }, [&](int it, double v) { av[it] = v; });
       ex.sync();
-      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+      lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, j = it % NX;
         double v = -rr[P.oX + it] + dh[it] * av[k * Nc];
         for (int c = 1; c < Nc; ++c) v -= fxv(P, ex, c - 1, j) * av[k * Nc + c];
@@ -1101,7 +1107,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       }, [&](int it, double v) { q0[it] = v; });
       ex.sync();
     } else {
-      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+      lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, j = it % NX;
         const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
         double v = -rr[P.oX + it];
@@ -1305,7 +1311,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     const gdouble* lvec = lv_ + ri * lstr;
     if (n0) {
       gdouble* nn = n0 + ri * ns;
-      lane_batch<4>(ex, 0, P.T * NX, [&](int it) {
+      lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
         double v = lvec[it];
 #pragma unroll
@@ -1313,7 +1319,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         return -v;
       }, [&](int it, double v) { nn[it] = v; });
     }
-    lane_batch<4>(ex, 0, P.T * Nc, [&](int it) {
+    lane_batch<BMPC_TS_UN>(ex, 0, P.T * Nc, [&](int it) {
       const int k = it / Nc, c = it % Nc;
       const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
       double fx = 0.0;
