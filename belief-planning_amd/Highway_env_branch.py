@@ -125,8 +125,8 @@ def Highway_sim(env, T):
                         a, b = env.veh_set[i], env.veh_set[j]
                         dis = max(abs(a.state[0] - b.state[0]) - 0.5 * (a.v_length + b.v_length),
                                   abs(a.state[1] - b.state[1]) - 0.5 * (a.v_width + b.v_width))
-            if dis < 0:       # the reference tests only the last pair's distance (:427)
-                collision = True
+                if dis < 0:   # after each i: the distance to vehicle i's last partner (:427-428)
+                    collision = True
         u_set, x_set, xx_set, xPred, zPred, branch_w = env.step(t)
         xPred_rec[t], zPred_rec[t], branch_w_rec[t] = xPred, zPred, branch_w
         for i in range(env.NV):
