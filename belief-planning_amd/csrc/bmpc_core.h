@@ -126,6 +126,8 @@ struct Plan {
   int nlds_lean;            // LDS doubles when the coupling system lives in the slab (Layout::coup)
   int lds_scr, nscr;       // tree-solve LDS scratch (slack terms of the pre-pass; 0 = none)
   int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
+  int maxq;   // largest cone dimension (fused cone passes hold a cone's rows in registers when
+              // maxq <= X::kConeRegRows * cgrp)
   double W1[BMPC_MAX_N * BMPC_MAX_N];   // sqrtm(Q) / chol(Q)'  (MPC_branch.py:1628-1631)
   double Wu[BMPC_MAX_D * BMPC_MAX_D];   // chol(R)'             (:1633-1636)
   double QQ[BMPC_MAX_N * BMPC_MAX_N];   // W1'W1

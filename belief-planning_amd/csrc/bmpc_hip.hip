@@ -51,6 +51,8 @@ struct DevExecT {
   static constexpr int nlanes = 64;
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
+  // cone rows per lane the fused IPM passes hold in registers (bmpc_ipm.h, cone_regs)
+  static constexpr int kConeRegRows = 8;
   __device__ double tsum(double v) const {
     v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]

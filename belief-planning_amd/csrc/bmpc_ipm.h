@@ -177,19 +177,90 @@ BMPC_HD double fx_coef(const Ctx& C, const X& ex, int k, int c, int j) {
   return fxv(P, ex, c - 1, j);
 }
 
-// out(rows) = G zv, cone rows boosted
-template <class X, int NX, int NU>
-BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out) {
+template <class X>
+BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out, double sw = 1.0,
+                     const gdouble* add = nullptr, double sa = 0.0);
+
+// Fused cone passes: a chain of whole-vector passes whose intermediate vectors were written
+// to the slab and read straight back becomes one pass that keeps each cone's rows in
+// registers (lane gl of the cone's group owns rows gl + uu*cg, uu < X::kConeRegRows).
+// Plans whose largest cone does not fit (P.maxq > kConeRegRows * cg) run the unfused chain.
+template <class X>
+BMPC_HD bool cone_regs(const X& ex, CPlan& P) {
+  const int cg = ex.nlanes == 1 ? 1 : P.cgrp;
+  return P.maxq <= X::kConeRegRows * cg;
+}
+
+// y = sc (2 a (a'v) - J v) over one cone's register rows (rows past q hold a = v = 0);
+// v0 = row 0 of v, known on every lane of the group
+template <int UC, class X>
+BMPC_HD void cone_W_regs(const X& ex, const ConeGroups& G, const double (&a)[UC], const double (&v)[UC], double v0,
+                         double sc, double (&y)[UC]) {
+  double part = 0.0;
+#pragma unroll
+  for (int uu = 0; uu < UC; ++uu) part += a[uu] * v[uu];
+  const double dot = ex.gsum(part, G.cg);
+#pragma unroll
+  for (int uu = 0; uu < UC; ++uu) {
+    const int i = G.gl + uu * G.cg;
+    y[uu] = sc * (2.0 * a[uu] * dot - (i == 0 ? v0 : -v[uu]));
+  }
+}
+
+// the NT vector of a cone in register rows: v (W, W^2 use v / wbar) or J v (inverses)
+template <int UC, class X>
+BMPC_HD void cone_a_regs(const ConeGroups& G, const gdouble* a, bool jconj, int off, int q, double (&av)[UC]) {
+#pragma unroll
+  for (int uu = 0; uu < UC; ++uu) {
+    const int i = G.gl + uu * G.cg;
+    const double t = a[off + (i < q ? i : 0)];
+    av[uu] = i < q ? ((jconj && i > 0) ? -t : t) : 0.0;
+  }
+}
+
+// row 0 of a register-held cone vector, broadcast to the group (lane gl = 0 owns it)
+template <int UC, class X>
+BMPC_HD double cone_row0(const X& ex, const ConeGroups& G, const double (&v)[UC]) {
+  return ex.gsum(G.gl == 0 ? v[0] : 0.0, G.cg);
+}
+
+// out(rows) = G zv, cone rows boosted.  WM = 1: out = W^-1 (G zv) - r3h, WM = 2: out =
+// W^-1 (W^-1 (G zv) - r3h) -- the tail of kkt_solve_once without the G dx vector in the slab
+// (tr: scratch of the unfused chain).
+template <class X, int NX, int NU, int WM = 0>
+BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out, const gdouble* r3h = nullptr,
+                             gdouble* tr = nullptr) {
   const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  if constexpr (WM > 0) {
+    r3h = uniform_ptr(r3h);
+    if (!cone_regs(ex, P)) {
+      apply_G<X, NX, NU, 0>(ex, C, zv, tr);
+      apply_W(ex, C, 1, tr, out, 1.0, r3h, -1.0);
+      if (WM == 2) apply_W(ex, C, 1, out, out);
+      return;
+    }
+  }
+  constexpr int UC = X::kConeRegRows;
   double qx[NX];
   ctx_qx<NX>(C, qx);
-  CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYG);
   BMPC_COUNT(C.ws, *C.L, PROF_NAPPLYG);
   BMPC_TIC(t_glp);
   const auto t = topo_view(P, ex);
   const int Nc = P.Nc;
   const gdouble* dh = C.at(C.L->dh);
+  const gdouble* dli = C.at(C.L->dli);
+  // LP rows: W^-1 = diag(1/d)
+  auto lp = [&](int row, double g) {
+    if constexpr (WM == 0) {
+      return g;
+    } else {
+      const double w = dli[row];
+      const double h = w * g - r3h[row];
+      return WM == 2 ? w * h : h;
+    }
+  };
   // Fx rows + positivity rows
   struct Two { double a, b; };
   // branch-free bodies: every load of a batch is issued before the first wait (a branch on
@@ -205,7 +276,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       const double fd = dh[k * NX + j], fx = fxv(P, ex, cr, j);
       v += (on * (c == 0 ? -fd : fx)) * zv[P.oX + k * NX + j];
     }
-    return Two{v, -S};
+    return Two{lp(P.rFx + it, v), lp(P.rPos + it, -S)};
   }, [&](int it, Two r) { out[P.rFx + it] = r.a; out[P.rPos + it] = r.b; });
   // Fu rows
   lane_batch(ex, 0, P.U * P.nFu, [&](int it) {
@@ -213,13 +284,15 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     double v = 0.0;
 #pragma unroll
     for (int j = 0; j < NU; ++j) v += P.desc.Fu[r * NU + j] * zv[P.oU + u * NU + j];
-    return v;
+    return lp(P.rFu + it, v);
   }, [&](int it, double v) { out[P.rFu + it] = v; });
   // risk rows: -rho, -mu+, -mu-
   lane_batch(ex, 0, P.bdim * (2 * P.m + 1), [&](int it) {
-    return it < P.bdim ? -zv[P.oRho + it] : -zv[P.oMup + (it - P.bdim)];
+    return lp(P.rRisk + it, it < P.bdim ? -zv[P.oRho + it] : -zv[P.oMup + (it - P.bdim)]);
   }, [&](int it, double v) { out[P.rRisk + it] = v; });
   const gdouble* boost = C.at(C.L->boost);
+  const gdouble* vn = C.at(C.L->vnt);
+  const gdouble* eta = C.at(C.L->eta);
   const double Qs = P.desc.Qslack[1];
   BMPC_TOC(C.ws, *C.L, PROF_G_LP, t_glp);
   BMPC_TIC(t_gcone);
@@ -234,6 +307,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     const int ndx = t.br_ndx[c0], ndu = t.br_ndu[c0];
     const bool hasch = t.br_child0[c0] >= 0;
     // first/last rows: +-e^-beta (F1 . zv), F1 spread over the group's lanes by node
+    double f;
     {
       // the root cone (c < 0) holds the root node's slacks only (ndx = br_ndx[0] = 0)
       const int nn = c >= 0 ? P.N : (k >= 0 ? 1 : 0);
@@ -258,16 +332,12 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       double acc = ex.gsum(part, G.cg);
       acc += tail;
       if (c >= 0 && hasch) acc += rho_c;
-      const double f = acc * ebst;
-      if (k >= 0 && G.gl == 0) {
-        out[off] = f;
-        out[off + q - 1] = -f;
-      }
+      f = acc * ebst;   // exact on the group's lane 0
     }
     // middle rows: rows are contiguous after each cone's first
     const int nxn = c >= 0 ? P.N * NX : 0;
     const int nmid = k < 0 ? 0 : c >= 0 ? P.N * (NX + NU) : NU;
-    strided_batch<4>(G.gl, G.cg, nmid, [&](int it) {
+    auto mid = [&](int it) {
       double v = 0.0;
       if (it < nxn) {
         const int j = it / NX, r = it % NX;
@@ -282,7 +352,48 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
         for (int s2 = 0; s2 < NU; ++s2) v += -2.0 * P.Wu[r * NU + s2] * zv[P.oU + uk * NU + s2];
       }
       return v;
-    }, [&](int it, double v) { out[off + 1 + it] = v; });
+    };
+    if constexpr (WM == 0) {
+      if (k >= 0 && G.gl == 0) {
+        out[off] = f;
+        out[off + q - 1] = -f;
+      }
+      strided_batch<4>(G.gl, G.cg, nmid, mid, [&](int it, double v) { out[off + 1 + it] = v; });
+    } else {
+      // the cone's rows of G zv in registers (q = nmid + 2), then W^-1 (and again for WM = 2)
+      const double f0 = ex.gsum(G.gl == 0 ? f : 0.0, G.cg);
+      double v[UC], a[UC], y[UC];
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = G.gl + uu * G.cg;
+        const int im = i >= 1 && i <= nmid ? i - 1 : 0;
+        const double m = mid(im);
+        v[uu] = i >= q ? 0.0 : i == 0 ? f0 : i == q - 1 ? -f0 : m;
+      }
+      cone_a_regs<UC, X>(G, vn, true, off, q, a);
+      const double sc = 1.0 / (k >= 0 ? eta[kk] : 1.0);
+      cone_W_regs<UC>(ex, G, a, v, f0, sc, y);
+#pragma unroll
+      for (int uu = 0; uu < UC; ++uu) {
+        const int i = G.gl + uu * G.cg;
+        y[uu] = i < q ? y[uu] - r3h[off + i] : 0.0;
+      }
+      if constexpr (WM == 2) {
+        const double y0 = cone_row0<UC>(ex, G, y);
+        cone_W_regs<UC>(ex, G, a, y, y0, sc, v);
+#pragma unroll
+        for (int uu = 0; uu < UC; ++uu) {
+          const int i = G.gl + uu * G.cg;
+          if (i < q) out[off + i] = v[uu];
+        }
+      } else {
+#pragma unroll
+        for (int uu = 0; uu < UC; ++uu) {
+          const int i = G.gl + uu * G.cg;
+          if (i < q) out[off + i] = y[uu];
+        }
+      }
+    }
   }
   BMPC_TOC(C.ws, *C.L, PROF_G_CONE, t_gcone);
   ex.sync();
@@ -614,8 +725,8 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
 // depends on its own input row and its cone's dot product, read before any write)
 // mode 0: W v, 1: W^-1 v, 2: W^2 v, 3: W^-2 v   (W symmetric NT scaling)
 template <class X>
-BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out, double sw = 1.0,
-                     const gdouble* add = nullptr, double sa = 0.0) {
+BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdouble* out, double sw,
+                     const gdouble* add, double sa) {
   CPlan& P = *C.P;
   BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
   const gdouble* dl = C.at((mode == 0 || mode == 2) ? C.L->dl : C.L->dli);   // d or 1/d
@@ -734,6 +845,304 @@ BMPC_FN_MAX_STEP double max_step(const X ex, const Ctx Cin, const gdouble* lam, 
   }
   a = ex.min(a);
   return ex.max(bad) > 0.0 ? 0.0 : a;
+}
+
+// both step lengths of an IPM step in one pass over lam: min(max_step(lam, d1), max_step(lam, d2))
+template <class X>
+BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam, const gdouble* d1, const gdouble* d2) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  struct A2 { double a, b; };
+  double a1 = 1e300, a2 = 1e300;
+  strided_batch<8>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
+    const double l = lam[i], u = d1[i], v = d2[i];
+    return A2{u < 0.0 ? -l / u : 1e300, v < 0.0 ? -l / v : 1e300};
+  }, [&](int, A2 r) { a1 = fmin(a1, r.a); a2 = fmin(a2, r.b); });
+  double bad = 0.0;
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    const double ln2 = cone_res(ex, G, lam, off, q);
+    if (!(ln2 > 0.0)) bad = 1.0;
+    const double ln = sqrt(ln2);
+    const double lb0 = q > 0 ? lam[off] / ln : 0.0;
+    auto one = [&](const gdouble* d, double& a) {
+      const double ld = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
+                                G.cg);
+      const double rho0 = q > 0 ? (lam[off] * d[off] - ld) / ln : 0.0;
+      const double fac = q > 0 ? (rho0 + d[off]) / (lb0 + 1.0) : 0.0;
+      const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
+        const double r1 = d[off + i] - fac * lam[off + i] / ln;
+        return r1 * r1;
+      }), G.cg);
+      const double tt = sqrt(ss) - rho0;
+      if (k >= 0 && tt > 0.0) a = fmin(a, ln / tt);
+    };
+    one(d1, a1);
+    one(d2, a2);
+  }
+  const double a = fmin(ex.min(a1), ex.min(a2));
+  return ex.max(bad) > 0.0 ? 0.0 : a;
+}
+
+// out1 = W^-1 in and out2 = W^-1 out1 in one pass (kkt_solve: r3h and the G' operand of
+// kkt_solve_once)
+template <class X>
+BMPC_HD void apply_Winv2(const X ex, const Ctx& C, const gdouble* in, gdouble* out1, gdouble* out2) {
+  CPlan& P = *C.P;
+  if (!cone_regs(ex, P)) {
+    apply_W(ex, C, 1, in, out1);
+    apply_W(ex, C, 1, out1, out2);
+    return;
+  }
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
+  constexpr int UC = X::kConeRegRows;
+  const gdouble* dli = C.at(C.L->dli);
+  struct Two { double a, b; };
+  lane_batch<8>(ex, 0, P.nlp, [&](int i) {
+    const double w = dli[i];
+    const double a = w * in[i];
+    return Two{a, w * a};
+  }, [&](int i, Two v) { out1[i] = v.a; out2[i] = v.b; });
+  const gdouble* vn = C.at(C.L->vnt);
+  const gdouble* eta = C.at(C.L->eta);
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    double a[UC], v[UC], y[UC];
+    cone_a_regs<UC, X>(G, vn, true, off, q, a);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      const double t = in[off + (i < q ? i : 0)];
+      v[uu] = i < q ? t : 0.0;
+    }
+    const double v0 = q > 0 ? in[off] : 0.0;
+    const double sc = 1.0 / (k >= 0 ? eta[k] : 1.0);
+    cone_W_regs<UC>(ex, G, a, v, v0, sc, y);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i < q) out1[off + i] = y[uu];
+    }
+    cone_W_regs<UC>(ex, G, a, y, cone_row0<UC>(ex, G, y), sc, v);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i < q) out2[off + i] = v[uu];
+    }
+  }
+  ex.sync();
+}
+
+// the affine step's directions in one pass: dz = z2 + t z1, rb = W dz, ds = -lam - rb
+template <class X>
+BMPC_HD void affine_dirs(const X ex, const Ctx& C, const gdouble* z2, const gdouble* z1, double t,
+                         const gdouble* lam, gdouble* rb, gdouble* ds) {
+  CPlan& P = *C.P;
+  if (!cone_regs(ex, P)) {
+    gdouble* dz = C.at(C.L->dz);
+    lane_batch<8>(ex, 0, P.nrows, [&](int i) { return z2[i] + t * z1[i]; }, [&](int i, double v) { dz[i] = v; });
+    ex.sync();
+    apply_W(ex, C, 0, dz, rb);
+    lane_batch<8>(ex, 0, P.nrows, [&](int i) { return -lam[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });
+    ex.sync();
+    return;
+  }
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
+  constexpr int UC = X::kConeRegRows;
+  const gdouble* dl = C.at(C.L->dl);
+  struct Two { double a, b; };
+  lane_batch<8>(ex, 0, P.nlp, [&](int i) {
+    const double r = dl[i] * (z2[i] + t * z1[i]);
+    return Two{r, -lam[i] - r};
+  }, [&](int i, Two v) { rb[i] = v.a; ds[i] = v.b; });
+  const gdouble* vn = C.at(C.L->vnt);
+  const gdouble* eta = C.at(C.L->eta);
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    double a[UC], v[UC], y[UC], l[UC];
+    cone_a_regs<UC, X>(G, vn, false, off, q, a);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      const int ic = off + (i < q ? i : 0);
+      const double d = z2[ic] + t * z1[ic];
+      l[uu] = lam[ic];
+      v[uu] = i < q ? d : 0.0;
+    }
+    const double v0 = q > 0 ? z2[off] + t * z1[off] : 0.0;
+    const double sc = k >= 0 ? eta[k] : 1.0;
+    cone_W_regs<UC>(ex, G, a, v, v0, sc, y);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i < q) {
+        rb[off + i] = y[uu];
+        ds[off + i] = -l[uu] - y[uu];
+      }
+    }
+  }
+  ex.sync();
+}
+
+// the combined step's directions in one pass: z2 += t z1 (dz), rb = W dz, ds -= rb (dsW) and
+// rc = W dsW (the s update)
+template <class X>
+BMPC_HD void combined_dirs(const X ex, const Ctx& C, gdouble* z2, const gdouble* z1, double t, gdouble* ds,
+                           gdouble* rb, gdouble* rc) {
+  CPlan& P = *C.P;
+  if (!cone_regs(ex, P)) {
+    lane_batch<8>(ex, 0, P.nrows, [&](int i) { return z2[i] + t * z1[i]; }, [&](int i, double v) { z2[i] = v; });
+    ex.sync();
+    apply_W(ex, C, 0, z2, rb);
+    lane_batch<8>(ex, 0, P.nrows, [&](int i) { return ds[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });
+    ex.sync();
+    apply_W(ex, C, 0, ds, rc);
+    return;
+  }
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
+  constexpr int UC = X::kConeRegRows;
+  const gdouble* dl = C.at(C.L->dl);
+  struct Four { double z, r, d, c; };
+  lane_batch<4>(ex, 0, P.nlp, [&](int i) {
+    const double w = dl[i];
+    const double z = z2[i] + t * z1[i];
+    const double r = w * z;
+    const double d = ds[i] - r;
+    return Four{z, r, d, w * d};
+  }, [&](int i, Four v) { z2[i] = v.z; rb[i] = v.r; ds[i] = v.d; rc[i] = v.c; });
+  const gdouble* vn = C.at(C.L->vnt);
+  const gdouble* eta = C.at(C.L->eta);
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    double a[UC], v[UC], y[UC], d[UC];
+    cone_a_regs<UC, X>(G, vn, false, off, q, a);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      const int ic = off + (i < q ? i : 0);
+      const double z = z2[ic] + t * z1[ic];
+      d[uu] = ds[ic];
+      v[uu] = i < q ? z : 0.0;
+    }
+    const double v0 = q > 0 ? z2[off] + t * z1[off] : 0.0;
+    const double sc = k >= 0 ? eta[k] : 1.0;
+    cone_W_regs<UC>(ex, G, a, v, v0, sc, y);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      d[uu] = i < q ? d[uu] - y[uu] : 0.0;
+      if (i < q) {
+        z2[off + i] = v[uu];
+        rb[off + i] = y[uu];
+        ds[off + i] = d[uu];
+      }
+    }
+    cone_W_regs<UC>(ex, G, a, d, cone_row0<UC>(ex, G, d), sc, v);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i < q) rc[off + i] = v[uu];
+    }
+  }
+  ex.sync();
+}
+
+// the combined step's right-hand side in one pass (ECOS, oracle/ecos_ipm.py): with
+// ds = dsW_aff and rb = W dz_aff on entry,
+//   r = -lam o lam - dsW_aff o W dz_aff + smu e,  ds <- xi = lam \ r,  rb <- eta1 rz - W xi
+template <class X>
+BMPC_HD void combined_rhs(const X ex, const Ctx& C, const gdouble* lam, gdouble* ds, gdouble* rb, const gdouble* rz,
+                          double smu, double eta1) {
+  CPlan& P = *C.P;
+  if (!cone_regs(ex, P)) {
+    gdouble* ra = C.at(C.L->ra);
+    gdouble* rc = C.at(C.L->rc);
+    jprod(ex, C, lam, lam, ra);
+    jprod(ex, C, ds, rb, rc);
+    lane_batch<8>(ex, 0, P.nrows, [&](int i) {
+      const double v = -ra[i] - rc[i];
+      return i < P.nlp ? v + smu : v;   // + sigma mu e on the LP rows
+    }, [&](int i, double v) { ra[i] = v; });
+    ex.sync();
+    for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[topo_view(P, ex).cone_off[k]] += smu;   // ... and cone heads
+    ex.sync();
+    jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
+    apply_W(ex, C, 0, ds, rb, -1.0, rz, eta1);               // eta1 rz - W xi
+    return;
+  }
+  BMPC_PROF(C.ws, *C.L, PROF_APPLYW);
+  constexpr int UC = X::kConeRegRows;
+  const gdouble* dl = C.at(C.L->dl);
+  struct Two { double a, b; };
+  lane_batch<8>(ex, 0, P.nlp, [&](int i) {
+    const double l = lam[i];
+    const double xi = (-(l * l) - ds[i] * rb[i] + smu) / l;
+    return Two{xi, -(dl[i] * xi) + eta1 * rz[i]};
+  }, [&](int i, Two v) { ds[i] = v.a; rb[i] = v.b; });
+  const gdouble* vn = C.at(C.L->vnt);
+  const gdouble* eta = C.at(C.L->eta);
+  BMPC_CONE_ROUNDS(ex, P, G) {
+    BMPC_CONE_K(P, G, k, off, q);
+    double l[UC], bw[UC], r[UC];
+    double pll = 0.0, pdr = 0.0;
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      const int ic = off + (i < q ? i : 0);
+      const double lv = lam[ic], dv = ds[ic], bv = rb[ic];
+      l[uu] = i < q ? lv : 0.0;
+      bw[uu] = i < q ? bv : 0.0;
+      r[uu] = i < q ? dv : 0.0;
+      pll += l[uu] * l[uu];
+      pdr += r[uu] * bw[uu];
+    }
+    const double l0 = q > 0 ? lam[off] : 1.0;
+    const double d0 = q > 0 ? ds[off] : 0.0, b0 = q > 0 ? rb[off] : 0.0;
+    const double dll = ex.gsum(pll, G.cg), ddr = ex.gsum(pdr, G.cg);
+    // r_i = -(lam o lam)_i - (dsW o W dz)_i for i > 0 (row 0 below)
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) r[uu] = -(l0 * l[uu] + l0 * l[uu]) - (d0 * bw[uu] + b0 * r[uu]);
+    const double r0 = -dll - ddr + smu;
+    // xi = lam \ r: rho = lam0^2 - |lam1|^2 (cone_res), x0 = (l0 r0 - lam1'r1) / rho
+    double amax = 0.0, aidx = 1e300, plr = 0.0;
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      const double a = fabs(l[uu]);
+      if (i >= 1 && i < q && a > amax) amax = a, aidx = (double)i;
+      if (i >= 1) plr += l[uu] * r[uu];
+    }
+    const double gm = ex.gmax(amax, G.cg);
+    const double kd = ex.gmin(amax == gm && aidx < 1e300 ? aidx : 1e300, G.cg);
+    const int kidx = kd < 1e300 ? (int)kd : -1;
+    double pss = 0.0;
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i >= 1 && i != kidx) pss += l[uu] * l[uu];
+    }
+    const double ss = ex.gsum(pss, G.cg), lr = ex.gsum(plr, G.cg);
+    const double rho = q > 0 ? cone_res_parts(l0, gm, ss) : 1.0;
+    const double x0 = q > 0 ? (l0 * r0 - lr) / rho : 0.0;
+    double a[UC];
+    cone_a_regs<UC, X>(G, vn, false, off, q, a);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      r[uu] = i >= q ? 0.0 : i == 0 ? x0 : (r[uu] - x0 * l[uu]) / l0;
+    }
+    const double sc = -(k >= 0 ? eta[k] : 1.0);
+    cone_W_regs<UC>(ex, G, a, r, x0, sc, l);
+#pragma unroll
+    for (int uu = 0; uu < UC; ++uu) {
+      const int i = G.gl + uu * G.cg;
+      if (i < q) {
+        ds[off + i] = r[uu];
+        rb[off + i] = l[uu] + eta1 * rz[off + i];
+      }
+    }
+  }
+  ex.sync();
 }
 
 // branches of depth dep are contiguous in BFS order: sum_{i<dep} m^i .. + m^dep
@@ -1479,14 +1888,14 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
 template <class X, int NX, int NU>
 BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
-                            const gdouble* r3h, gdouble* dx, gdouble* dy, gdouble* dzh) {
+                            const gdouble* r3h, gdouble* dx, gdouble* dy, gdouble* dzh, bool tr_ready, bool fin) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
   gdouble* ws = C.ws;
   gdouble* tr = ws + L.k_r0;
   gdouble* tz = ws + L.k_nv0;
-  apply_W(ex, C, 1, r3h, tr);                     // W^-1 r3h
+  if (!tr_ready) apply_W(ex, C, 1, r3h, tr);      // W^-1 r3h (kkt_solve forms it with r3h)
   apply_GT<X, NX, NU>(ex, C, tr, tz, r1);         // G' W^-1 r3h + r1
   tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
@@ -1540,9 +1949,9 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
     else dy[P.T * NX + i - ng] = b[i];
   }
   ex.sync();
-  // dzh = W^-1 G dx - r3h
-  apply_G<X, NX, NU>(ex, C, dx, tr);
-  apply_W(ex, C, 1, tr, dzh, 1.0, r3h, -1.0);
+  // dzh = W^-1 G dx - r3h, or (fin) dz = W^-1 dzh, in one pass
+  if (fin) apply_G<X, NX, NU, 2>(ex, C, dx, dzh, r3h, tr);
+  else apply_G<X, NX, NU, 1>(ex, C, dx, dzh, r3h, tr);
 }
 
 // Solve [0 A' G'; A 0 0; G 0 -W^2] [dx; dy; dz] = [r1; r2; r3]: W-scaled solve with
@@ -1564,9 +1973,12 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
   gdouble* cy = ws + L.k_cy;
   gdouble* cz = ws + L.k_cz;
   gdouble* tv = ws + L.k_nv1;
-  apply_W(ex, C, 1, r3, r3h);
+  apply_Winv2(ex, C, r3, r3h, ws + L.k_r0);      // r3h = W^-1 r3 and kkt_solve_once's W^-1 r3h
   BMPC_COUNT(ws, L, PROF_NSOLVE);
-  kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz);   // dz holds dzh until the end
+  // without refinement the solve's tail applies the final W^-1 itself
+  const bool fin = ex.uniform(nitref == 0);
+  kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz, true, fin);   // dz holds dzh until the end
+  if (fin) return;
   const double sc = nitref == 0 ? 0.0 : ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
                                      strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
                                 strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
@@ -1592,7 +2004,7 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
     if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
-    kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz);
+    kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz, false, false);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
     lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });
     lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[i] + cz[i]; }, [&](int i, double v) { dz[i] = v; });
@@ -1854,31 +2266,19 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2, nref);
       const double dk_aff = -kap * tau;
       const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
-      lane_batch<8>(ex, 0, nr, [&](int i) { return z2[i] + dtau_a * z1[i]; }, [&](int i, double v) { dz[i] = v; });
-      ex.sync();
-      apply_W(ex, C, 0, dz, rb);                               // W dz_aff
-      lane_batch<8>(ex, 0, nr, [&](int i) { return -lam[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW_aff = xi - W dz_aff
-      ex.sync();
+      // dz_aff = z2 + dtau_a z1, rb = W dz_aff, ds = dsW_aff = xi - W dz_aff (one pass)
+      affine_dirs(ex, C, z2, z1, dtau_a, lam, rb, ds);
       const double dkap_a = (dk_aff - kap * dtau_a) / tau;
-      double a_aff = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
+      double a_aff = max_step2(ex, C, lam, ds, rb);
       if (dtau_a < 0.0) a_aff = fmin(a_aff, -tau / dtau_a);
       if (dkap_a < 0.0) a_aff = fmin(a_aff, -kap / dkap_a);
       a_aff = fmax(0.0, fmin(a_aff, 0.999));
       double sigma = (1.0 - a_aff) * (1.0 - a_aff) * (1.0 - a_aff);
       sigma = fmin(1.0, fmax(1e-4, sigma));
       const double eta1 = 1.0 - sigma;
-      // combined: ds_comb = -lam o lam - dsW_a o Wdz_a + sigma mu e
-      jprod(ex, C, lam, lam, ra);
-      jprod(ex, C, ds, rb, rc);
-      lane_batch<8>(ex, 0, nr, [&](int i) {
-        const double v = -ra[i] - rc[i];
-        return i < P.nlp ? v + (sigma * mu) : v;   // + sigma mu e on the LP rows
-      }, [&](int i, double v) { ra[i] = v; });
-      ex.sync();
-      for (int k = ex.lane; k < P.ncones; k += ex.nlanes) ra[topo_view(P, ex).cone_off[k]] += sigma * mu;   // ... and cone heads
-      ex.sync();
-      jdiv(ex, C, lam, ra, ds);                                // xi (kept in ds)
-      apply_W(ex, C, 0, ds, rb, -1.0, rz, eta1);               // eta1 rz - W xi
+      // combined: ds_comb = -lam o lam - dsW_a o Wdz_a + sigma mu e, xi = lam \ ds_comb (kept in
+      // ds), rb = eta1 rz - W xi (one pass)
+      combined_rhs(ex, C, lam, ds, rb, rz, sigma * mu, eta1);
       lane_batch<16>(ex, 0, nv, [&](int i) { return -eta1 * rx[i]; }, [&](int i, double v) { tA[i] = v; });
       lane_batch(ex, 0, neq, [&](int i) { return eta1 * ry[i]; }, [&](int i, double v) { ya[i] = v; });
       ex.sync();
@@ -1891,25 +2291,22 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
         if (!isfinite(v)) nonfinite = 1.0;
       });
       lane_batch(ex, 0, neq, [&](int i) { return y2[i] + (dtau * y1[i]); }, [&](int i, double v) { y2[i] = v; });
-      lane_batch<8>(ex, 0, nr, [&](int i) { return z2[i] + (dtau * z1[i]); }, [&](int i, double v) { z2[i] = v; });
       ex.sync();
-      apply_W(ex, C, 0, z2, rb);                               // W dz
-      lane_batch<8>(ex, 0, nr, [&](int i) { return ds[i] - rb[i]; }, [&](int i, double v) { ds[i] = v; });   // dsW
-      ex.sync();
+      // dz = z2 + dtau z1, rb = W dz, ds = dsW = xi - W dz, rc = W dsW = ds (one pass)
+      combined_dirs(ex, C, z2, z1, dtau, ds, rb, rc);
       dkap = (dk_c - kap * dtau) / tau;
-      double a = fmin(max_step(ex, C, lam, ds), max_step(ex, C, lam, rb));
+      double a = max_step2(ex, C, lam, ds, rb);
       if (dtau < 0.0) a = fmin(a, -tau / dtau);
       if (dkap < 0.0) a = fmin(a, -kap / dkap);
       a = fmin(a, 0.999);
       alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
-      apply_W(ex, C, 0, ds, rb);                               // ds = W dsW
       const double fin = ex.max(nonfinite);
       ok = ex.uniform(fin == 0.0 && isfinite(dtau) && alpha > 1e-10);
       if (ok) {
         lane_batch<8>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
         lane_batch(ex, 0, neq, [&](int i) { return y[i] + (alpha * y2[i]); }, [&](int i, double v) { y[i] = v; });
         struct ZS { double z, s; };
-        lane_batch<4>(ex, 0, nr, [&](int i) { return ZS{z[i] + alpha * z2[i], s[i] + alpha * rb[i]}; },
+        lane_batch<4>(ex, 0, nr, [&](int i) { return ZS{z[i] + alpha * z2[i], s[i] + alpha * rc[i]}; },
                    [&](int i, ZS v) { z[i] = v.z; s[i] = v.s; });
         tau += alpha * dtau;
         kap += alpha * dkap;

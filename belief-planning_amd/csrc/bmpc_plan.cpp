@@ -279,6 +279,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   hp.u_cone[0] = k;
   row += 2 + d;
   P.nrows = row;
+  P.maxq = 0;
+  for (int q : hp.cone_q) P.maxq = q > P.maxq ? q : P.maxq;
   if (desc.controller != BMPC_CTRL_CVAR) {
     // BranchMPCProx's / BranchMPC's OSQP vector z = [X | U | S] and rows [Fx-type | Fu | -S] (MPC_branch.py:185-370)
     P.oS = T * n + U * d;

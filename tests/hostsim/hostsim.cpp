@@ -30,6 +30,7 @@ struct HostExecT {
   const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
   double* eco = nullptr;      // ... and for the per-ego constants (kTransform)
   static constexpr int kTaskLanes = 1;
+  static constexpr int kConeRegRows = 256;   // one lane holds a whole cone (fused IPM passes)
   double tsum(double v) const { return v; }
   template <int S>
   double tget(double v) const { return v; }
