@@ -57,6 +57,9 @@
 #ifndef BMPC_FN_TREE_SOLVE
 #define BMPC_FN_TREE_SOLVE BMPC_FN
 #endif
+#ifndef BMPC_FN_FUSED
+#define BMPC_FN_FUSED BMPC_FN   // the fused cone passes (out of line: -0.8% k_ipm vs inlined, A/B at 4096 egos)
+#endif
 
 namespace bmpc {
 
@@ -225,8 +228,8 @@ BMPC_HD double cone_row0(const X& ex, const ConeGroups& G, const double (&v)[UC]
 }
 
 // out(rows) = G zv, cone rows boosted.  WM = 1: out = W^-1 (G zv) - r3h, WM = 2: out =
-// W^-1 (W^-1 (G zv) - r3h) -- the tail of kkt_solve_once without the G dx vector in the slab
-// (tr: scratch of the unfused chain).
+// W^-1 (W^-1 (G zv) - r3h), WM = 3: out = W^-1 (G zv) -- the tail of kkt_solve_once without the
+// G dx vector in the slab (tr: scratch of the unfused chain).
 template <class X, int NX, int NU, int WM = 0>
 BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out, const gdouble* r3h = nullptr,
                              gdouble* tr = nullptr) {
@@ -236,7 +239,8 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     r3h = uniform_ptr(r3h);
     if (!cone_regs(ex, P)) {
       apply_G<X, NX, NU, 0>(ex, C, zv, tr);
-      apply_W(ex, C, 1, tr, out, 1.0, r3h, -1.0);
+      if (WM == 3) apply_W(ex, C, 1, tr, out);
+      else apply_W(ex, C, 1, tr, out, 1.0, r3h, -1.0);
       if (WM == 2) apply_W(ex, C, 1, out, out);
       return;
     }
@@ -257,6 +261,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       return g;
     } else {
       const double w = dli[row];
+      if (WM == 3) return w * g;
       const double h = w * g - r3h[row];
       return WM == 2 ? w * h : h;
     }
@@ -376,7 +381,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
         const int i = G.gl + uu * G.cg;
-        y[uu] = i < q ? y[uu] - r3h[off + i] : 0.0;
+        if (WM != 3) y[uu] = i < q ? y[uu] - r3h[off + i] : 0.0;
       }
       if constexpr (WM == 2) {
         const double y0 = cone_row0<UC>(ex, G, y);
@@ -887,7 +892,9 @@ BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam,
 // out1 = W^-1 in and out2 = W^-1 out1 in one pass (kkt_solve: r3h and the G' operand of
 // kkt_solve_once)
 template <class X>
-BMPC_HD void apply_Winv2(const X ex, const Ctx& C, const gdouble* in, gdouble* out1, gdouble* out2) {
+BMPC_FN_FUSED void apply_Winv2(const X ex, const Ctx Cin, const gdouble* in, gdouble* out1, gdouble* out2) {
+  const Ctx C = Cin.uniform();
+  in = uniform_ptr(in), out1 = uniform_ptr(out1), out2 = uniform_ptr(out2);
   CPlan& P = *C.P;
   if (!cone_regs(ex, P)) {
     apply_W(ex, C, 1, in, out1);
@@ -935,8 +942,10 @@ BMPC_HD void apply_Winv2(const X ex, const Ctx& C, const gdouble* in, gdouble* o
 
 // the affine step's directions in one pass: dz = z2 + t z1, rb = W dz, ds = -lam - rb
 template <class X>
-BMPC_HD void affine_dirs(const X ex, const Ctx& C, const gdouble* z2, const gdouble* z1, double t,
-                         const gdouble* lam, gdouble* rb, gdouble* ds) {
+BMPC_FN_FUSED void affine_dirs(const X ex, const Ctx Cin, const gdouble* z2, const gdouble* z1, double t,
+                               const gdouble* lam, gdouble* rb, gdouble* ds) {
+  const Ctx C = Cin.uniform();
+  z2 = uniform_ptr(z2), z1 = uniform_ptr(z1), lam = uniform_ptr(lam), rb = uniform_ptr(rb), ds = uniform_ptr(ds);
   CPlan& P = *C.P;
   if (!cone_regs(ex, P)) {
     gdouble* dz = C.at(C.L->dz);
@@ -987,8 +996,10 @@ BMPC_HD void affine_dirs(const X ex, const Ctx& C, const gdouble* z2, const gdou
 // the combined step's directions in one pass: z2 += t z1 (dz), rb = W dz, ds -= rb (dsW) and
 // rc = W dsW (the s update)
 template <class X>
-BMPC_HD void combined_dirs(const X ex, const Ctx& C, gdouble* z2, const gdouble* z1, double t, gdouble* ds,
-                           gdouble* rb, gdouble* rc) {
+BMPC_FN_FUSED void combined_dirs(const X ex, const Ctx Cin, gdouble* z2, const gdouble* z1, double t, gdouble* ds,
+                                 gdouble* rb, gdouble* rc) {
+  const Ctx C = Cin.uniform();
+  z2 = uniform_ptr(z2), z1 = uniform_ptr(z1), ds = uniform_ptr(ds), rb = uniform_ptr(rb), rc = uniform_ptr(rc);
   CPlan& P = *C.P;
   if (!cone_regs(ex, P)) {
     lane_batch<8>(ex, 0, P.nrows, [&](int i) { return z2[i] + t * z1[i]; }, [&](int i, double v) { z2[i] = v; });
@@ -1051,8 +1062,10 @@ BMPC_HD void combined_dirs(const X ex, const Ctx& C, gdouble* z2, const gdouble*
 // ds = dsW_aff and rb = W dz_aff on entry,
 //   r = -lam o lam - dsW_aff o W dz_aff + smu e,  ds <- xi = lam \ r,  rb <- eta1 rz - W xi
 template <class X>
-BMPC_HD void combined_rhs(const X ex, const Ctx& C, const gdouble* lam, gdouble* ds, gdouble* rb, const gdouble* rz,
-                          double smu, double eta1) {
+BMPC_FN_FUSED void combined_rhs(const X ex, const Ctx Cin, const gdouble* lam, gdouble* ds, gdouble* rb,
+                                const gdouble* rz, double smu, double eta1) {
+  const Ctx C = Cin.uniform();
+  lam = uniform_ptr(lam), ds = uniform_ptr(ds), rb = uniform_ptr(rb), rz = uniform_ptr(rz);
   CPlan& P = *C.P;
   if (!cone_regs(ex, P)) {
     gdouble* ra = C.at(C.L->ra);
@@ -1886,7 +1899,8 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
 // One pass of the W-scaled KKT system (oracle/ecos_ipm.py KKT)
 //   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
-template <class X, int NX, int NU>
+// R3ZERO: r3h = 0 (refinement corrections): G'W^-1 r3h + r1 = r1 feeds the tree solve directly
+template <class X, int NX, int NU, bool R3ZERO = false>
 BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const gdouble* r2,
                             const gdouble* r3h, gdouble* dx, gdouble* dy, gdouble* dzh, bool tr_ready, bool fin) {
   const Ctx C = Cin.uniform();
@@ -1895,8 +1909,12 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   gdouble* ws = C.ws;
   gdouble* tr = ws + L.k_r0;
   gdouble* tz = ws + L.k_nv0;
-  if (!tr_ready) apply_W(ex, C, 1, r3h, tr);      // W^-1 r3h (kkt_solve forms it with r3h)
-  apply_GT<X, NX, NU>(ex, C, tr, tz, r1);         // G' W^-1 r3h + r1
+  if constexpr (R3ZERO) {
+    tz = const_cast<gdouble*>(r1);
+  } else {
+    if (!tr_ready) apply_W(ex, C, 1, r3h, tr);    // W^-1 r3h (kkt_solve forms it with r3h)
+    apply_GT<X, NX, NU>(ex, C, tr, tz, r1);       // G' W^-1 r3h + r1
+  }
   tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   auto* b = coup_mem(ex, ws, L, P, P.lds_rhs);
@@ -1950,7 +1968,8 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   }
   ex.sync();
   // dzh = W^-1 G dx - r3h, or (fin) dz = W^-1 dzh, in one pass
-  if (fin) apply_G<X, NX, NU, 2>(ex, C, dx, dzh, r3h, tr);
+  if constexpr (R3ZERO) apply_G<X, NX, NU, 3>(ex, C, dx, dzh, r3h, tr);
+  else if (fin) apply_G<X, NX, NU, 2>(ex, C, dx, dzh, r3h, tr);
   else apply_G<X, NX, NU, 1>(ex, C, dx, dzh, r3h, tr);
 }
 
@@ -1995,8 +2014,8 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
     apply_A<X, NX, NU>(ex, C, dx, e2);
     lane_batch(ex, 0, P.neq, [&](int i) { return r2[i] - e2[i]; }, [&](int i, double v) { e2[i] = v; });
     // e3 = r3h - W^-1 G dx + dzh is zero up to rounding: kkt_solve_once computed dzh as
-    // W^-1 G dx - r3h from the final dx with the same operators
-    lane_batch<16>(ex, 0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { e3[i] = v; });
+    // W^-1 G dx - r3h from the final dx with the same operators (the correction solve takes
+    // r3h = 0 without a vector)
     ex.sync();
     const double err = ex.max(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(e1[i]); }),
                                    strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(e2[i]); })));
@@ -2004,7 +2023,7 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
     if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
-    kkt_solve_once<X, NX, NU>(ex, C, e1, e2, e3, cx, cy, cz, false, false);
+    kkt_solve_once<X, NX, NU, true>(ex, C, e1, e2, nullptr, cx, cy, cz, false, false);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
     lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });
     lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[i] + cz[i]; }, [&](int i, double v) { dz[i] = v; });
