@@ -20,5 +20,6 @@ for tag in os.environ["VARS"].split()[1:]:
         np.max(np.abs(a["upred"][:, 0] - b["upred"][:, 0]))))
 PY
 bash tools/exp_batch.sh "4096" $VARS $VARS || exit 1
+[ -n "$SKIP_TESTS" ] && exit 0
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1
 tail -5 gpurun_out/ab_tests.log
