@@ -144,57 +144,6 @@ BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const
 }
 
 // ------------------------------------------------------------------------------------
-// acc[a][b] = g_{k0+a}' v_b over the tree variables (a < na <= 4, b < nb <= 4, v_b = v + b*vs),
-// reading each g_k (and the v_b) only on g_k's
-// support (kkt_factor): the x / u / S entries of the cone's branch (N nodes), or the root
-// node's S and u entries for the root cone -- a quarter to a third of the vector instead of
-// all of it.
-// ------------------------------------------------------------------------------------
-template <class X, int NX, int NU>
-BMPC_HD void cone_gdots(const X ex, CPlan& P, const gdouble* gk, const gdouble* v, size_t vs, int nb, int k0, int na,
-                        double (&acc)[4][4]) {
-  const auto t = topo_view(P, ex);
-  const int Nc = P.Nc, lx = P.N * NX, lu = P.N * NU, lmax = P.N * (NX + NU + Nc);
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-  struct Term { double p[4]; int a; };
-  lane_batch<4>(ex, 0, na * lmax, [&](int it) {
-    const int a = it / lmax, j = it % lmax, k = k0 + a;
-    const int c = t.cone_c[k];
-    const int c0 = c >= 0 ? c : 0;
-    const int ndx = c >= 0 ? t.br_ndx[c0] : 0, ndu = c >= 0 ? t.br_ndu[c0] : 0;
-    int i;
-    bool on;
-    if (c >= 0) {
-      on = true;
-      i = j < lx ? P.oX + ndx * NX + j : j < lx + lu ? P.oU + ndu * NU + (j - lx) : P.oS + ndx * Nc + (j - lx - lu);
-    } else {   // root cone: the root node's S entries, then its u entries
-      on = j < Nc + NU;
-      i = j < Nc ? P.oS + j : P.oU + (j - Nc < NU ? j - Nc : 0);
-    }
-    const double g = on ? gk[(size_t)k * P.nv + i] : 0.0;
-    Term r;
-    r.a = a;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) r.p[b] = b < nb ? g * v[b * vs + i] : 0.0;
-    return r;
-  }, [&](int, Term r) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if (r.a == a) acc[a][b] += r.p[b];
-  });
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (a < na && b < nb) acc[a][b] = ex.sum(acc[a][b]);
-}
-
-// ------------------------------------------------------------------------------------
 // reductions over one cone's rows, by the cone group G that owns the cone (k >= 0) or as an
 // idle member (k < 0, q = 0): every lane of the wave must make the same calls.
 // ------------------------------------------------------------------------------------
@@ -1894,6 +1843,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
   const gdouble* eta = ws + L.eta;
   const gdouble* dl = ws + L.dl;
   const gdouble* p = ws + L.p;
+  const int ntree = P.oRho;    // x and u parts are [0, oRho); S part [oS, oJ)
   for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
   ex.sync();
   // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables,
@@ -1902,7 +1852,8 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
     for (int j0 = 0; j0 < nc; j0 += 4) {
       const int na = nc - k0 < 4 ? nc - k0 : 4, nbk = nc - j0 < 4 ? nc - j0 : 4;
       double acc[4][4];
-      cone_gdots<X, NX, NU>(ex, P, ws + L.gk, ws + L.colk + (size_t)j0 * P.nv, P.nv, nbk, k0, na, acc);
+      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, ws + L.colk + (size_t)j0 * P.nv, P.nv, nbk,
+                 0, ntree, P.oS, P.oJ, acc);
       if (ex.lane == 0)
         for (int a = 0; a < na; ++a) {
           const int k = k0 + a;
@@ -1975,7 +1926,7 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
     const int na = nc - k0 < 4 ? nc - k0 : 4;
     double acc[4][4];
-    cone_gdots<X, NX, NU>(ex, P, ws + L.gk, dx, 0, 1, k0, na, acc);
+    block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
     if (ex.lane == 0)
       for (int a = 0; a < na; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
   }
