@@ -18,6 +18,10 @@
 
 using namespace bmpc;
 
+#ifndef BMPC_HOST_CONE_REGS
+#define BMPC_HOST_CONE_REGS 256
+#endif
+
 namespace {
 template <bool TR, bool CL = true>
 struct HostExecT {
@@ -30,7 +34,9 @@ struct HostExecT {
   const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
   double* eco = nullptr;      // ... and for the per-ego constants (kTransform)
   static constexpr int kTaskLanes = 1;
-  static constexpr int kConeRegRows = 256;   // one lane holds a whole cone (fused IPM passes)
+  // one lane holds a whole cone (fused IPM passes); -DBMPC_HOST_CONE_REGS=1 runs the unfused
+  // chain instead (what the GPU takes for cones wider than 8 rows per group lane)
+  static constexpr int kConeRegRows = BMPC_HOST_CONE_REGS;
   double tsum(double v) const { return v; }
   template <int S>
   double tget(double v) const { return v; }

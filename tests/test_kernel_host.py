@@ -94,3 +94,24 @@ def test_lean_lds_path_matches(monkeypatch):
         out.append(hs.solve(rb["x"], rb["z"], rb["xref"]))
     for k in ("status", "iters", "J", "upred"):
         np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+def test_unfused_cone_chain_replays_reference():
+    """The fused cone passes (bmpc_ipm.h) fall back to the unfused chain of whole-vector passes
+    for cones wider than the registers hold (the GPU's NB = 2 plans).  A host build with one
+    register row per lane takes that chain for every cone; it must replay the reference's
+    recorded closed loops like the fused build (same tolerances)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path[:0] = [%r, %r, %r]\n"
+        "import test_kernel_host as t\n"
+        "t.test_host_build_replays_reference('highway_n10_nb1', 20)\n"
+        "t.test_host_build_replays_reference('highway_n8_nb2', 40)\n"
+        "import hostsim_lib; assert 'CONE_REGS' in hostsim_lib.SO, hostsim_lib.SO\n"
+        "print('ok')\n") % (os.path.dirname(__file__), os.path.dirname(os.path.dirname(__file__)),
+                             os.path.join(os.path.dirname(os.path.dirname(__file__)), "belief-planning_amd"))
+    env = dict(os.environ, BMPC_HOSTSIM_FLAGS="-DBMPC_HOST_CONE_REGS=1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
