@@ -132,13 +132,21 @@ class BranchMPC_CVaR:
         self._last = None
 
     # ---- plan ------------------------------------------------------------------------------
+    def _takes_transform(self):
+        """Plans of this controller accept solve's S / Fx / bx (MPC_branch.py:2043-2057): the
+        CVaR controller over the highway models (HIGHWAY plans get BMPC_PLAN_TRANSFORM, the
+        merge model always has it)."""
+        kind = getattr(self.predictiveModel, "model_kind", None)
+        return self.controller_kind == abi.CTRL_CVAR and kind in (abi.MODEL_HIGHWAY, abi.MODEL_HIGHWAY_MERGE)
+
     def plan_desc(self):
         mdl = self.predictiveModel
         Fx = np.asarray(self.Fx, float).reshape(-1, self.n)
+        flags = abi.PLAN_TRANSFORM if (self._takes_transform() and mdl.model_kind == abi.MODEL_HIGHWAY) else 0
         return abi.make_desc(self.controller_kind, mdl.model_kind, self.n, self.d, self.N, self.NB, self.m,
                              mdl.dt, self.Q, self.R, Fx, _flat_bx(self.bx), self.Fu,
                              np.asarray(self.bu, float).reshape(-1), self.Qslack, mdl.model_constants(),
-                             ralpha=self.ralpha, Qf=self.Qf, dR=self.dR)
+                             ralpha=self.ralpha, Qf=self.Qf, dR=self.dR, flags=flags)
 
     def _ensure_plan(self):
         if self._plan is None:
@@ -151,33 +159,37 @@ class BranchMPC_CVaR:
         return self._plan
 
     # ---- solve -----------------------------------------------------------------------------
-    def _transform(self, pl, S, bx, B):
-        """The S / bx arguments of solve (MPC_branch.py:2052-2057): S is reset on every call,
-        bx kept when None.  Only the merge model's plans take them (bmpc_set_transform)."""
-        merge = getattr(self.predictiveModel, "model_kind", None) == abi.MODEL_HIGHWAY_MERGE
-        if not merge:
-            if S is not None or bx is not None:
-                raise NotImplementedError("a state transformation S / per-step bx needs the merge model "
-                                          "(highway_branch_dyn.PredictiveModel_merge)")
+    def _transform(self, pl, S, Fx, bx, B):
+        """The S / Fx / bx arguments of solve (MPC_branch.py:2052-2057): S is reset on every
+        call, Fx and bx are kept when None.  The state rows they form follow the reference's
+        build / update split (bmpc_set_transform, include/bmpc.h)."""
+        if not self._takes_transform():
+            if S is not None or Fx is not None or bx is not None:
+                raise NotImplementedError("solve's S / Fx / bx need the CVaR controller over a highway model")
             return
+        if Fx is not None:
+            F = np.asarray(Fx, float).reshape(-1, self.n)
+            if F.shape[0] != np.asarray(self.param.Fx, float).reshape(-1, self.n).shape[0]:
+                raise ValueError("a per-step Fx must keep the row count of mpcParameters.Fx")
+            pl.set_fx(np.broadcast_to(F, (B,) + F.shape))
         S_arr = None if S is None else np.broadcast_to(np.asarray(S, float), (B, self.n, self.n))
         bx_arr = None if bx is None else np.broadcast_to(_flat_bx(bx), (B, _flat_bx(bx).size))
         pl.set_transform(S_arr, bx_arr)
 
     def solve(self, x, z, xRef=None, S=None, Fx=None, bx=None):
-        """One controller step (MPC_branch.py:2043-2092); S / bx: the merge scene's state
-        transformation and state bound (PredictiveModel_merge controllers)."""
-        if Fx is not None:
-            raise NotImplementedError("a per-step Fx (no reference scene passes one)")
+        """One controller step (MPC_branch.py:2043-2092), including solve's S (state
+        transformation), Fx and bx (state constraints)."""
         if self.batch != 1:
             raise ValueError("this controller holds a batch; use solve_batch")
         if xRef is not None:
             self.xRef = xRef
         self.S = S
+        if Fx is not None:
+            self.Fx = Fx
         if bx is not None:
             self.bx = bx
         pl = self._ensure_plan()
-        self._transform(pl, S, bx, 1)
+        self._transform(pl, S, Fx, bx, 1)
         t0 = datetime.datetime.now()
         r = pl.solve(np.asarray(x, float)[None], np.asarray(z, float)[None],
                      np.asarray(self.xRef, float)[None])
@@ -199,12 +211,12 @@ class BranchMPC_CVaR:
         self._bt = None            # rebuilt from the device tree on first access of .BT
         self._tree = None
 
-    def solve_batch(self, X, Z, XREF, S=None, bx=None):
+    def solve_batch(self, X, Z, XREF, S=None, bx=None, Fx=None):
         """Batched step for all egos of the plan: returns the raw result dict
-        (upred [B,U,d], xpred [B,T,n], branch_w, J, status, iters); S [B,n,n] / bx [B,nFx]
-        as in solve (merge model)."""
+        (upred [B,U,d], xpred [B,T,n], branch_w, J, status, iters); S [B,n,n], bx [B,nFx],
+        Fx [B,nFx,n] (or one for all) as in solve."""
         pl = self._ensure_plan()
-        self._transform(pl, S, bx, self.batch)
+        self._transform(pl, S, Fx, bx, self.batch)
         t0 = datetime.datetime.now()
         r = pl.solve(X, Z, XREF)
         self.solverTime = datetime.datetime.now() - t0
@@ -216,6 +228,8 @@ class BranchMPC_CVaR:
     def _tree_arrays(self, e=0):
         if getattr(self, "_tree", None) is None:
             self._tree = self._plan.tree()
+            if self.tree_index.bdim > 0 and self.controller_kind != abi.CTRL_ROBUST:
+                self._tree["dp"] = self._plan.branch_dp()
         return {k: v[e] for k, v in self._tree.items()}
 
     def BT2array(self, e=0):
@@ -261,6 +275,7 @@ class BranchMPC_CVaR:
                             t.depth[b])
             if not t.is_leaf(b):
                 br.p = a["p"][b].copy()
+                br.dp = a["dp"][b].copy()      # (m, n), MPC_branch.py:1711,1842
             nodes.append(br)
         for b in range(t.nbranch):
             for c in t.children[b]:

@@ -69,6 +69,7 @@ _SIGS = {
     "bmpc_plan_info": (C.c_int, [C.c_void_p, C.c_void_p]),
     "bmpc_set_policies": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_reset": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "bmpc_get_policies": (C.c_int, [C.c_void_p, C.c_void_p]),
     "bmpc_solve": (C.c_int, [C.c_void_p] + [C.c_void_p] * 9),
     "bmpc_solve_device": (C.c_int, [C.c_void_p] + [C.c_void_p] * 10),
     "bmpc_get_tree": (C.c_int, [C.c_void_p] + [C.c_void_p] * 6),
@@ -78,6 +79,8 @@ _SIGS = {
     "bmpc_get_robust_warm_start": (C.c_int, [C.c_void_p] * 4),
     "bmpc_set_robust_warm_start": (C.c_int, [C.c_void_p] * 5),
     "bmpc_set_transform": (C.c_int, [C.c_void_p] * 5),
+    "bmpc_set_fx": (C.c_int, [C.c_void_p] * 3),
+    "bmpc_get_branch_dp": (C.c_int, [C.c_void_p] * 2),
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),

@@ -9,6 +9,7 @@ MAX_N, MAX_D, MAX_FX, MAX_FU, MAX_M = 8, 4, 8, 8, 4
 
 CTRL_CVAR, CTRL_PROX, CTRL_QP, CTRL_ROBUST = 0, 1, 2, 3
 MODEL_HIGHWAY, MODEL_QUADRUPED, MODEL_HIGHWAY_MERGE = 0, 1, 2
+PLAN_TRANSFORM = 1      # bmpc_plan_desc.flags: solve's S / Fx / bx on a HIGHWAY CVaR plan
 POL_MAINTAIN, POL_BRAKE, POL_LC, POL_MAINTAIN_TRACKV, POL_FORWARD, POL_STOP = range(6)
 
 (INFO_T, INFO_U, INFO_BDIM, INFO_NBRANCH, INFO_NV, INFO_NEQ, INFO_NROWS, INFO_NCONES,
@@ -38,6 +39,7 @@ class PlanDesc(C.Structure):
         ("Qslack", C.c_double * 2),
         ("mc", C.c_double * 8),
         ("feastol", C.c_double), ("abstol", C.c_double), ("reltol", C.c_double),
+        ("flags", C.c_int32), ("reserved_flags", C.c_int32),
     ]
 
 
@@ -71,7 +73,7 @@ def _fill(arr, values):
 
 def make_desc(controller, model, n, d, N, NB, m, dt, Q, R, Fx, bx, Fu, bu, Qslack,
               mc, ralpha=0.9, Qf=None, dR=None, maxit=100,
-              feastol=1e-8, abstol=1e-8, reltol=1e-8) -> PlanDesc:
+              feastol=1e-8, abstol=1e-8, reltol=1e-8, flags=0) -> PlanDesc:
     """Pack a plan description (all matrices row-major at their logical size)."""
     Fx = np.asarray(Fx, float).reshape(-1, n)
     Fu = np.asarray(Fu, float).reshape(-1, d)
@@ -94,6 +96,7 @@ def make_desc(controller, model, n, d, N, NB, m, dt, Q, R, Fx, bx, Fu, bu, Qslac
     _fill(D.Qslack, Qslack)
     _fill(D.mc, mc)
     D.feastol, D.abstol, D.reltol = feastol, abstol, reltol
+    D.flags = int(flags)
     return D
 
 

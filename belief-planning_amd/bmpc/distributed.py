@@ -8,9 +8,13 @@ from __future__ import annotations
 
 import os
 
-# layout of the statistics vector (float64)
-STAT_J, STAT_J2, STAT_INFEAS, STAT_ITERS, STAT_SOLVES, STAT_COLL = range(6)
+# layout of the statistics vector (float64): the per-ego closed-loop statistics of bmpc_env.h
+# (ENVS_*) summed over egos -- slot 6 is then the NUMBER of egos that collided -- and one flag
+# slot, "some ego collided", reduced with MAX (sum, and max for flags)
+STAT_J, STAT_J2, STAT_INFEAS, STAT_ITERS, STAT_SOLVES, STAT_COLL_STEPS, STAT_COLLIDED, STAT_ANY_COLLIDED = range(8)
+STAT_COLL = STAT_COLL_STEPS
 NSTAT = 8
+MAX_SLOTS = (STAT_ANY_COLLIDED,)
 
 
 def world():
@@ -37,11 +41,25 @@ def init(backend: str = "nccl", device=None):
     return rank, local, ws
 
 
-def reduce_stats(stats):
-    """Sum the per-rank statistics vector in place (RCCL on GPU tensors, gloo on CPU)."""
+def episode_stats(per_ego):
+    """A rank's statistics vector from its per-ego rows [B, NSTAT] (torch or NumPy): sums over
+    the egos, and the flag slot set when any ego collided."""
+    out = per_ego.sum(0)
+    out[STAT_ANY_COLLIDED] = per_ego[:, STAT_COLLIDED].max() if per_ego.shape[0] else 0.0
+    return out
+
+
+def reduce_stats(stats, max_slots=MAX_SLOTS):
+    """Reduce the per-rank statistics vector in place over the ranks (RCCL on GPU tensors,
+    gloo on CPU): SUM for the sums, MAX for the flag slots."""
     import torch.distributed as dist
     if dist.is_initialized() and dist.get_world_size() > 1:
+        idx = list(max_slots)
+        flags = stats[idx].clone()
         dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        if idx:
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+            stats[idx] = flags
     return stats
 
 

@@ -62,6 +62,14 @@ class BatchPlan:
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         check(lib().bmpc_set_policies(self._h, arr, _p(m)), "bmpc_set_policies")
 
+    def get_policies(self):
+        """The policies in force, per ego m (kind, params) tuples -- including the device-side
+        lane-change re-targets of env_step_device."""
+        arr = (abi.Policy * (self.batch * self.desc.m))()
+        check(lib().bmpc_get_policies(self._h, arr), "bmpc_get_policies")
+        m = self.desc.m
+        return [[(int(arr[e * m + i].kind), tuple(arr[e * m + i].p)) for i in range(m)] for e in range(self.batch)]
+
     def reset(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         check(lib().bmpc_reset(self._h, _p(m)), "bmpc_reset")
@@ -118,13 +126,28 @@ class BatchPlan:
     def set_transform(self, S=None, bx=None, s_on=None, mask=None):
         """Per-ego state transformation S [B,n,n] (None = "S is None" for every ego) and
         state bound bx [B,nFx] (None = keep) of the next solves -- the S / bx arguments of
-        BranchMPC_CVaR.solve (MPC_branch.py:2043-2057); HIGHWAY_MERGE plans only."""
+        BranchMPC_CVaR.solve (MPC_branch.py:2043-2057); HIGHWAY_MERGE plans and HIGHWAY CVaR
+        plans created with abi.PLAN_TRANSFORM."""
         B, n = self.batch, self.desc.n
         S = None if S is None else np.ascontiguousarray(np.asarray(S, np.float64).reshape(B, n, n))
         bx = None if bx is None else np.ascontiguousarray(np.asarray(bx, np.float64).reshape(B, self.desc.nFx))
         on = None if s_on is None else np.ascontiguousarray(s_on, np.uint8)
         m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
         check(lib().bmpc_set_transform(self._h, _p(S), _p(on), _p(bx), _p(m)), "bmpc_set_transform")
+
+    def set_fx(self, Fx, mask=None):
+        """Per-ego state-constraint matrix Fx [B,nFx,n] of the next solves -- the Fx argument of
+        BranchMPC_CVaR.solve (MPC_branch.py:2055-2056), kept until the next one; transform
+        plans only (bmpc_set_fx)."""
+        Fx = np.ascontiguousarray(np.asarray(Fx, np.float64).reshape(self.batch, self.desc.nFx, self.desc.n))
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        check(lib().bmpc_set_fx(self._h, _p(Fx), _p(m)), "bmpc_set_fx")
+
+    def branch_dp(self):
+        """BranchTree.dp (d p / d x) of every non-leaf branch of the last solve [B,bdim,m,n]."""
+        out = np.zeros((self.batch, self.bdim, self.desc.m, self.desc.n))
+        check(lib().bmpc_get_branch_dp(self._h, _p(out)), "bmpc_get_branch_dp")
+        return out
 
     def get_robust_warm_start(self):
         """robustMPC's warm start: xLin [B,T,n], uLin [B,U,d], OldInput [B,d]."""

@@ -95,9 +95,15 @@ typedef const BMPC_AS_LDS int32_t lint;
 typedef TopoT<gint*> Topo;
 typedef TopoT<lint*> TopoL;
 
-// transform slots (Layout::xform): S row-major, bx, "S is not None", "bx was set"
+// transform slots (Layout::xform): S row-major, the current bx (solve's bx argument), "S is
+// not None", "bx was set", the current Fx (solve's Fx argument), "Fx was set", and the state
+// rows / bound the solves use -- written on the first solve and on solves with S on, kept
+// otherwise (buildIneqConstr :1894-1901 vs updateIneqConstr :2016-2036) -- and "rows written"
+// (an ego resumed through the warm-start ABI has none yet: its next solve writes them)
 enum { XF_S = 0, XF_BX = BMPC_MAX_N * BMPC_MAX_N, XF_SON = XF_BX + BMPC_MAX_FX, XF_BXSET = XF_SON + 1,
-       XF_COUNT = XF_BXSET + 1 };
+       XF_FX = XF_BXSET + 1, XF_FXSET = XF_FX + BMPC_MAX_FX * BMPC_MAX_N, XF_ROWS = XF_FXSET + 1,
+       XF_BROWS = XF_ROWS + BMPC_MAX_FX * BMPC_MAX_N, XF_ROWSET = XF_BROWS + BMPC_MAX_FX,
+       XF_COUNT = XF_ROWSET + 1 };
 
 // Per-ego constants of a transform-capable solve (X::kTransform), formed once per solve in
 // the wave's LDS: Fx S, W1 S, (W1 S)'(W1 S) and bx (MPC_branch.py:1894-1901,1935-1937);
@@ -176,7 +182,7 @@ struct Layout {
   // persistent state (survives between solves)
   size_t uLin, pprev, misc, xpred, upred, sol;
   // tree of the current solve
-  size_t xbar, zbar, ubar, Ad, Bd, Cd, dh, h0, w, p, boost, xref;
+  size_t xbar, zbar, ubar, Ad, Bd, Cd, dh, h0, w, p, dp, boost, xref;
   // IPM vectors
   size_t x, y, z, s, lam, x1, y1, z1, x2, y2, z2, dz, ds, rx, ry, rz, hvec, bvec;
   size_t ta, ya, ra, rb, rc, bestx;

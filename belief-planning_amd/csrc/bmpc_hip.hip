@@ -131,12 +131,13 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
 // waves per SIMD).  Deep trees (N=30, NB=2: 17 KB of tables, a 20 KB coupling matrix) run
 // lean, 16 egos per CU instead of 4, unless the batch is resident either way.  BMPC_LDS_RICH=0/1
 // forces either.
-static bool choose_lds_rich(const Plan& P, bool transform, int batch) {
+static bool choose_lds_rich(const Plan& P, bool transform, int batch, int cus, size_t lds_per_cu) {
   if (const char* e = getenv("BMPC_LDS_RICH")) return atoi(e) != 0;
-  auto egos = [](size_t b) { return std::min<size_t>(16, (160 * 1024) / std::max<size_t>(b, 1)); };
+  auto egos = [&](size_t b) { return std::min<size_t>(16, lds_per_cu / std::max<size_t>(b, 1)); };
   const size_t rich = egos(solver_lds_bytes(P, transform, true));
-  // a batch that is resident either way (256 CUs) runs rich: residency is not what limits it
-  return (size_t)batch <= 256 * rich || rich >= egos(solver_lds_bytes(P, transform, false));
+  // a batch that is resident either way (one CU per `rich` egos) runs rich: residency is not
+  // what limits it
+  return (size_t)batch <= (size_t)cus * rich || rich >= egos(solver_lds_bytes(P, transform, false));
 }
 
 template <class M>
@@ -284,6 +285,12 @@ __global__ __launch_bounds__(64) void k_bandqp(BandQPDesc d, const double* __res
   if (threadIdx.x == 0) status[b] = st;
 }
 
+// plans whose solves take S / Fx / bx (bmpc_set_transform, bmpc_set_fx)
+bool plan_takes_transform(const Plan& P) {
+  return P.desc.model == BMPC_MODEL_HIGHWAY_MERGE ||
+         (P.desc.model == BMPC_MODEL_HIGHWAY && (P.desc.flags & BMPC_PLAN_TRANSFORM));
+}
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -323,6 +330,8 @@ hipError_t upload(DevBuf& b, const void* host, size_t bytes) {
 
 struct bmpc_ctx {
   int device;
+  int cus;             // compute units (hipDeviceProp_t::multiProcessorCount)
+  size_t lds_per_cu;   // LDS bytes per CU (maxSharedMemoryPerMultiProcessor)
 };
 
 struct bmpc_plan {
@@ -363,7 +372,11 @@ int bmpc_open(int hip_device, bmpc_ctx** out) {
   HIPCHECK(hipGetDeviceCount(&ndev));
   if (hip_device < 0 || hip_device >= ndev) return fail(-19, "no such HIP device");
   HIPCHECK(hipSetDevice(hip_device));
-  *out = new bmpc_ctx{hip_device};
+  hipDeviceProp_t prop;
+  HIPCHECK(hipGetDeviceProperties(&prop, hip_device));
+  const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  const size_t lds = prop.maxSharedMemoryPerMultiProcessor > 0 ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
+  *out = new bmpc_ctx{hip_device, cus, lds};
   return 0;
 }
 
@@ -477,6 +490,15 @@ int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask
   return 0;
 }
 
+int bmpc_get_policies(bmpc_plan* pl, bmpc_policy* pol) {
+  if (!pl || !pol) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  HIPCHECK(hipStreamSynchronize(pl->stream));
+  if (pl->user_stream) HIPCHECK(hipStreamSynchronize(pl->user_stream));
+  HIPCHECK(hipMemcpy(pol, pl->d_pol, sizeof(bmpc_policy) * pl->h_pol.size(), hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int bmpc_reset(bmpc_plan* pl, const uint8_t* mask) {
   if (!pl) return fail(-22, "null argument");
   HIPCHECK(hipSetDevice(pl->ctx->device));
@@ -527,19 +549,25 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const Plan& P = pl->hp.plan;
   const int B = pl->batch;
   const bool merge = P.desc.model == BMPC_MODEL_HIGHWAY_MERGE;
-  const bool tl = choose_lds_rich(P, merge, B);
-  size_t lds_bytes = solver_lds_bytes(P, merge, tl);
+  // HIGHWAY plans that take solve's S / Fx / bx run the transform path of the same model
+  const bool hwt = P.desc.model == BMPC_MODEL_HIGHWAY && (P.desc.flags & BMPC_PLAN_TRANSFORM);
+  const bool xform = merge || hwt;
+  const bool tl = choose_lds_rich(P, xform, B, pl->ctx->cus, pl->ctx->lds_per_cu);
+  size_t lds_bytes = solver_lds_bytes(P, xform, tl);
   // occupancy experiments: BMPC_IPM_LDS_BYTES reserves at least that much LDS per workgroup
   // (fewer egos resident per CU => a smaller working set in L2 / Infinity Cache)
   if (const char* e = getenv("BMPC_IPM_LDS_BYTES")) {
     const size_t want = (size_t)atol(e);
-    if (want > lds_bytes && want <= 160 * 1024) lds_bytes = want;
+    if (want > lds_bytes && want <= pl->ctx->lds_per_cu) lds_bytes = want;
   }
   if (pl->timing && (pl->t_pending < 0 || pl->t_pending >= bmpc_plan::kTimeSlots))
     return fail(-5, "timing ring out of range (t_pending = " + std::to_string(pl->t_pending) + ")");
   hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));
-  if (P.desc.model == BMPC_MODEL_HIGHWAY)
+  if (hwt)
+    hipLaunchKernelGGL(k_tree<HighwayT>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
+                       d_x, d_z, d_xref, B);
+  else if (P.desc.model == BMPC_MODEL_HIGHWAY)
     hipLaunchKernelGGL(k_tree<Highway>, dim3(B), dim3(64), 0, s, pl->d_bundle, pl->d_ws, pl->d_pol,
                        d_x, d_z, d_xref, B);
   else if (merge)
@@ -551,10 +579,19 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   HIPCHECK(hipGetLastError());
   if (pl->timing) HIPCHECK(hipEventRecord(ev[1], s));
   const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
+  // dynamic LDS above 64 KB needs the per-kernel opt-in (as k_bandqp does)
 #define BMPC_LAUNCH_SOLVER(KERNEL)                                                                  \
-  hipLaunchKernelGGL(KERNEL, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol, d_upred, \
-                     d_xpred, d_bw, d_J, d_status, d_iters, B)
-  if (P.desc.model == BMPC_MODEL_HIGHWAY) {
+  do {                                                                                              \
+    if (lds_bytes > 64 * 1024)                                                                      \
+      HIPCHECK(hipFuncSetAttribute((const void*)(KERNEL), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   (int)lds_bytes));                                                \
+    hipLaunchKernelGGL(KERNEL, dim3(B), dim3(64), lds_bytes, s, pl->d_bundle, pl->d_ws, pl->d_pol, d_upred, \
+                       d_xpred, d_bw, d_J, d_status, d_iters, B);                                   \
+  } while (0)
+  if (hwt) {
+    if (tl) BMPC_LAUNCH_SOLVER((k_ipm<HighwayT, true>));
+    else BMPC_LAUNCH_SOLVER((k_ipm<HighwayT, false>));
+  } else if (P.desc.model == BMPC_MODEL_HIGHWAY) {
     if (tl) BMPC_LAUNCH_SOLVER((qp ? k_qp<Highway, true> : k_ipm<Highway, true>));
     else BMPC_LAUNCH_SOLVER((qp ? k_qp<Highway, false> : k_ipm<Highway, false>));
   } else if (merge) {
@@ -727,8 +764,9 @@ int bmpc_set_robust_warm_start(bmpc_plan* pl, const double* xLin, const double* 
 int bmpc_set_transform(bmpc_plan* pl, const double* S, const uint8_t* s_on, const double* bx, const uint8_t* mask) {
   if (!pl) return fail(-22, "null argument");
   const Plan& P = pl->hp.plan;
-  if (P.desc.model != BMPC_MODEL_HIGHWAY_MERGE)
-    return fail(-22, "bmpc_set_transform: only HIGHWAY_MERGE plans take a state transformation");
+  if (!plan_takes_transform(P))
+    return fail(-22, "bmpc_set_transform: only HIGHWAY_MERGE plans and HIGHWAY CVaR plans created with "
+                     "BMPC_PLAN_TRANSFORM take a state transformation");
   HIPCHECK(hipSetDevice(pl->ctx->device));
   const Layout& L = pl->hp.lay;
   const int B = pl->batch, n = P.n, nF = P.nFx;
@@ -751,6 +789,30 @@ int bmpc_set_transform(bmpc_plan* pl, const double* S, const uint8_t* s_on, cons
     if (int rc = scatter_rows(pl, ones.data(), L.xform + XF_BXSET, 1, dmask.as<uint8_t>())) return rc;
   }
   return 0;
+}
+
+int bmpc_set_fx(bmpc_plan* pl, const double* Fx, const uint8_t* mask) {
+  if (!pl || !Fx) return fail(-22, "null argument");
+  const Plan& P = pl->hp.plan;
+  if (!plan_takes_transform(P))
+    return fail(-22, "bmpc_set_fx: only HIGHWAY_MERGE plans and HIGHWAY CVaR plans created with "
+                     "BMPC_PLAN_TRANSFORM take a per-solve Fx");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Layout& L = pl->hp.lay;
+  const int B = pl->batch;
+  DevBuf dmask;
+  HIPCHECK(upload(dmask, mask, B));
+  std::vector<double> ones(B, 1.0);
+  if (int rc = scatter_rows(pl, Fx, L.xform + XF_FX, P.nFx * P.n, dmask.as<uint8_t>())) return rc;
+  return scatter_rows(pl, ones.data(), L.xform + XF_FXSET, 1, dmask.as<uint8_t>());
+}
+
+int bmpc_get_branch_dp(bmpc_plan* pl, double* dp) {
+  if (!pl || !dp) return fail(-22, "null argument");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  const Plan& P = pl->hp.plan;
+  if (P.bdim * P.m * P.n == 0) return 0;
+  return gather(pl, pl->hp.lay.dp, P.bdim * P.m * P.n, dp);
 }
 
 int bmpc_get_tree(bmpc_plan* pl, double* xbar, double* ubar, double* zbar, double* w, double* p,
@@ -890,7 +952,7 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
                   int32_t* info) {
   if (!ctx || !q || !x || !status) return fail(-22, "null argument");
   HostBandQP h;
-  std::string err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, h);
+  std::string err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, h, ctx->cus, ctx->lds_per_cu);
   if (!err.empty()) return fail(-22, err);
   const int nnzP = Pp[n], nnzA = Ap[n];
   if ((nnzP && !Px) || (nnzA && !Ax)) return fail(-22, "null value array");

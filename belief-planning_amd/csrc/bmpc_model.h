@@ -353,6 +353,13 @@ struct HighwayMerge : Highway {
   }
 };
 
+// HighwayT: the highway model in a plan that takes solve's S / Fx / bx (BMPC_PLAN_TRANSFORM;
+// MPC_branch.py:2043-2057 accepts them for any model): same model functions, the per-ego
+// transform path of the solver (kTransform).
+struct HighwayT : Highway {
+  static constexpr bool kTransform = true;
+};
+
 // ------------------------------------------------------------------------------------
 // Quadruped: x = (X, Y, theta), u = (vx, vy, omega)   quadruped_branch_dyn.py:14-248
 // ------------------------------------------------------------------------------------

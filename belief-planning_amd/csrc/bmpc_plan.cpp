@@ -105,8 +105,11 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
     if (n != 4 || d != 2) return "highway model needs n=4, d=2";
     if (desc.model == BMPC_MODEL_HIGHWAY_MERGE && desc.controller != BMPC_CTRL_CVAR)
       return "the merge model (state transformation S) is supported with the CVaR controller";
+    if ((desc.flags & BMPC_PLAN_TRANSFORM) && desc.controller != BMPC_CTRL_CVAR)
+      return "BMPC_PLAN_TRANSFORM (solve's S / Fx / bx) needs the CVaR controller";
   } else if (desc.model == BMPC_MODEL_QUADRUPED) {
     if (n != 3 || d != 3) return "quadruped model needs n=3, d=3";
+    if (desc.flags & BMPC_PLAN_TRANSFORM) return "BMPC_PLAN_TRANSFORM is supported for the highway models";
   } else {
     return "unknown model";
   }
@@ -370,6 +373,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.h0 = take((size_t)T * P.Ncol);
   L.w = take(nbr);
   L.p = take((size_t)bd * m);
+  L.dp = take((size_t)bd * m * n);
   L.boost = take(nc);
   L.xref = take(n);
   L.x = take(nv);

@@ -17,9 +17,9 @@ int classify(double lo, double hi) {
   return (fu ? ROW_UP : 0) | (fl ? ROW_LO : 0);
 }
 
-std::string fmt(const char* f, long a, long b = 0) {
+std::string fmt(const char* f, long a, long b = 0, long c = 0) {
   char buf[256];
-  std::snprintf(buf, sizeof buf, f, a, b);
+  std::snprintf(buf, sizeof buf, f, a, b, c);
   return buf;
 }
 
@@ -107,7 +107,8 @@ void HostBandQP::point_tables(const int32_t* base) {
 }
 
 std::string bandqp_analyse(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap, const int32_t* Ai,
-                           int batch, const double* l, const double* u, int max_iter, double eps, HostBandQP& out) {
+                           int batch, const double* l, const double* u, int max_iter, double eps, HostBandQP& out,
+                           int cus, size_t lds_per_cu) {
   if (n < 1 || m < 0 || batch < 1) return "need n >= 1, m >= 0, batch >= 1";
   if (!Pp || !Ap || (m > 0 && (!l || !u))) return "null pattern or bounds";
   if (max_iter < 1 || !(eps > 0)) return "need max_iter >= 1 and eps > 0";
@@ -182,10 +183,10 @@ std::string bandqp_analyse(int n, int m, const int32_t* Pp, const int32_t* Pi, c
     for (int w : adj[v]) bw = std::max(bw, std::abs(pos[v] - pos[w]));
   const int W = bw + 1;
   const size_t lds_bytes = bandqp_lds_doubles(nk, W, false) * sizeof(double);
-  if (lds_bytes > 160 * 1024)
-    return fmt("KKT bandwidth %ld after reverse Cuthill-McKee ordering (dimension %ld) needs more than the 160 KB "
+  if (lds_bytes > lds_per_cu)
+    return fmt("KKT bandwidth %ld after reverse Cuthill-McKee ordering (dimension %ld) needs more than the %ld KB "
                "LDS of a CU for the factorisation window",
-               bw, nk);
+               bw, nk, (long)(lds_per_cu / 1024));
 
   HostBandQP& h = out;
   h = HostBandQP();
@@ -238,7 +239,7 @@ std::string bandqp_analyse(int n, int m, const int32_t* Pp, const int32_t* Pi, c
   d.max_iter = max_iter;
   // the factor in LDS when it fits and the batch is small enough to have a CU per problem
   // anyway (a 100 KB workgroup leaves one problem per CU: 2.7x fewer solves/s at 4096)
-  d.lb_lds = batch <= 256 && bandqp_lds_doubles(nk, W, true) * sizeof(double) <= 160 * 1024 ? 1 : 0;
+  d.lb_lds = batch <= cus && bandqp_lds_doubles(nk, W, true) * sizeof(double) <= lds_per_cu ? 1 : 0;
   d.eps = eps;
   d.stride = bandqp_stride(nk, W);
   for (auto* v : {&h.kind, &h.scat, &h.cscat, &h.xmap, &h.ymap}) h.blob.insert(h.blob.end(), v->begin(), v->end());

@@ -25,6 +25,7 @@ constexpr double kQPInfinity = 1e20;
 // of every problem (they must classify every row alike), then build everything.  Returns
 // "" on success, else an error message.
 std::string bandqp_analyse(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap, const int32_t* Ai,
-                           int batch, const double* l, const double* u, int max_iter, double eps, HostBandQP& out);
+                           int batch, const double* l, const double* u, int max_iter, double eps, HostBandQP& out,
+                           int cus = 256, size_t lds_per_cu = 160 * 1024);
 
 }  // namespace bmpc

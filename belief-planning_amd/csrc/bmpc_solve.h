@@ -27,22 +27,39 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
     ws[L.misc + MISC_JCONS] = j;
   }
   if constexpr (X::kTransform) {
-    // per-ego constants of this solve (MPC_branch.py:1894-1901,1935-1937): Fx S, W1 S,
-    // (W1 S)'(W1 S) when S is not None, else the plan's Fx, W1, QQ; the current bx
-    const double* xf = ws + L.xform;
-    const bool son = xf[XF_SON] != 0.0, bxset = xf[XF_BXSET] != 0.0;
+    // per-ego constants of this solve.  State rows and their bound: Fx S / bx (Fx without S)
+    // from the current Fx and bx, written by buildIneqConstr on the first solve
+    // (MPC_branch.py:1894-1901) and by updateIneqConstr only while S is on (:2025-2036) --
+    // with S off a later solve keeps the rows it finds (:2016-2024 patch the collision row
+    // alone).  The cone rows use W1 S (W1 without S) on every solve (:1935-1937, :1995-1998).
+    double* xf = ws + L.xform;
+    const bool son = xf[XF_SON] != 0.0, bxset = xf[XF_BXSET] != 0.0, fxset = xf[XF_FXSET] != 0.0;
+    const bool rewrite = !init || son || xf[XF_ROWSET] == 0.0;
     const double* S = xf + XF_S;
     const int nF = P.nFx;
+    if (rewrite) {
+      for (int i = ex.lane; i < nF * NX + nF; i += ex.nlanes) {
+        if (i < nF * NX) {
+          const int r = i / NX, j = i % NX;
+          const double* Fr = fxset ? xf + XF_FX + r * NX : P.desc.Fx + r * NX;
+          double v = Fr[j];
+          if (son) {
+            v = 0.0;
+            for (int k = 0; k < NX; ++k) v += Fr[k] * S[k * NX + j];
+          }
+          xf[XF_ROWS + i] = v;
+        } else {
+          const int r = i - nF * NX;
+          xf[XF_BROWS + r] = bxset ? xf[XF_BX + r] : P.desc.bx[r];
+        }
+      }
+      ex.sync();
+      if (ex.lane == 0) xf[XF_ROWSET] = 1.0;
+    }
     for (int i = ex.lane; i < nF * NX + 2 * NX * NX + nF; i += ex.nlanes) {
       double v;
       if (i < nF * NX) {
-        const int r = i / NX, j = i % NX;
-        v = P.desc.Fx[r * NX + j];
-        if (son) {
-          v = 0.0;
-          for (int k = 0; k < NX; ++k) v += P.desc.Fx[r * NX + k] * S[k * NX + j];
-        }
-        ex.eco[ECO_FX + i] = v;
+        ex.eco[ECO_FX + i] = xf[XF_ROWS + i];
       } else if (i < nF * NX + NX * NX) {
         const int q = i - nF * NX, r = q / NX, j = q % NX;
         v = P.W1[r * NX + j];
@@ -68,7 +85,7 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
         ex.eco[ECO_QQ + q] = v;
       } else {
         const int r = i - nF * NX - 2 * NX * NX;
-        ex.eco[ECO_BX + r] = bxset ? xf[XF_BX + r] : P.desc.bx[r];
+        ex.eco[ECO_BX + r] = xf[XF_BROWS + r];
       }
     }
   }

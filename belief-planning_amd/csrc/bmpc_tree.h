@@ -80,7 +80,8 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
       const int b = b0 + it / (m + 1), i = it % (m + 1) - 1;
       const int last = t.br_ndx[b] + t.br_len[b] - 1;
       if (i < 0) {
-        branch_eval<M>(mc, dt, N, m, E.pol, xbar + last * n, zbar + last * n, p + b * m, nullptr);
+        branch_eval<M>(mc, dt, N, m, E.pol, xbar + last * n, zbar + last * n, p + b * m,
+                       ws + L.dp + (size_t)b * m * n);   // BranchTree.dp (:1711, :1842)
       } else {
         const int c = t.br_child0[b] + i;
         rollout<M>(dt, N, E.pol[i], zbar + last * n, zbar + t.br_ndx[c] * n, n);

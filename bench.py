@@ -306,8 +306,8 @@ def main():
     for _ in range(a.steps):
         step()
         it_sum.add_(it)
-    stats = estats.sum(0)
-    D.reduce_stats(stats)        # the only collective
+    stats = D.episode_stats(estats)
+    D.reduce_stats(stats)        # the only collective: SUM, MAX for the flag
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -372,6 +372,8 @@ def main():
                             "iters_mean": float(st_h[abi.ENVS_ITERS] / max(st_h[abi.ENVS_SOLVES], 1)),
                             "solves": int(st_h[abi.ENVS_SOLVES]),
                             "collision_steps": int(st_h[abi.ENVS_COLL_STEPS]),
+                            "collided_egos": int(st_h[D.STAT_COLLIDED]),
+                            "any_collided": bool(st_h[D.STAT_ANY_COLLIDED] > 0),
                             "env": "device k_env (sim_overtake scene)" if not quad else "torch ops"},
         }
         if not a.no_cpu_baseline and world == 1 and not (quad or robust):

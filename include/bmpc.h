@@ -18,6 +18,9 @@
  *                         (BMPC_CTRL_PROX: OSQP QP, status 1 = solved / -2 = not)
  *                         (tree update, linearisation, assembly, ecos.solve / OSQP, unpack)
  *   bmpc_get_tree      <- BranchTree fields + BT2array    MPC_branch.py:65-78,2108-2122
+ *   bmpc_get_branch_dp <- BranchTree.dp                    MPC_branch.py:1711,1842
+ *   bmpc_set_transform <- solve(..., S, bx) arguments      MPC_branch.py:2043-2057
+ *   bmpc_set_fx        <- solve(..., Fx) argument          MPC_branch.py:2055-2056
  *   bmpc_model_eval    <- PredictiveModel.dyn_linearization / branch_eval / zpred_eval /
  *                         col_eval                         highway_branch_dyn.py:284-325
  *   bmpc_env_step      <- Highway_env.step + Highway_sim collision rule
@@ -42,7 +45,7 @@
 extern "C" {
 #endif
 
-#define BMPC_ABI_VERSION 1
+#define BMPC_ABI_VERSION 2
 
 #define BMPC_MAX_N 8      /* state dimension            */
 #define BMPC_MAX_D 4      /* input dimension            */
@@ -114,7 +117,16 @@ typedef struct {
    *   quadruped {L1, W1, L2, W2, col_tol, s1} (Quad_constants)                       */
   double mc[8];
   double feastol, abstol, reltol; /* ECOS tolerances (defaults 1e-8)              */
+  int32_t flags;        /* BMPC_PLAN_* (ABI 2)                            */
+  int32_t reserved_flags;
 } bmpc_plan_desc;
+
+/* plan flags */
+enum {
+  BMPC_PLAN_TRANSFORM = 1  /* CVaR plans of the HIGHWAY model that accept the per-solve S / Fx / bx
+                              arguments of BranchMPC_CVaR.solve (bmpc_set_transform, bmpc_set_fx);
+                              HIGHWAY_MERGE plans always do */
+};
 
 typedef struct bmpc_ctx bmpc_ctx;
 typedef struct bmpc_plan bmpc_plan;
@@ -147,6 +159,9 @@ int bmpc_plan_info(const bmpc_plan* plan, int32_t* info /* [BMPC_INFO_COUNT] */)
 
 /* update_backup: policies[batch][m]; mask[batch] (NULL = all egos) */
 int bmpc_set_policies(bmpc_plan* plan, const bmpc_policy* policies, const uint8_t* mask);
+/* the policies in force [batch][m], including the device-side lane-change re-targets of
+ * bmpc_env_step (update_backup, Highway_env_branch.py:117-118) */
+int bmpc_get_policies(bmpc_plan* plan, bmpc_policy* policies);
 /* forget the warm start (next solve runs inittree); mask NULL = all egos */
 int bmpc_reset(bmpc_plan* plan, const uint8_t* mask);
 
@@ -187,24 +202,36 @@ int bmpc_set_warm_start(bmpc_plan* plan, const double* uLin, const double* p,
                         const double* jcons, const double* old_input, const uint8_t* mask);
 
 /* Per-ego state transformation S and state bound bx of the next solves: the S / bx arguments
- * of BranchMPC_CVaR.solve(x, z, xRef, S, Fx=None, bx) (MPC_branch.py:2043-2057), used by the
- * merge scene (Highway_env_branch.py:358-367).  HIGHWAY_MERGE plans only.
+ * of BranchMPC_CVaR.solve(x, z, xRef, S, Fx, bx) (MPC_branch.py:2043-2057), used by the merge
+ * scene (Highway_env_branch.py:358-367).  HIGHWAY_MERGE plans and HIGHWAY CVaR plans created
+ * with BMPC_PLAN_TRANSFORM.
  *   S    [batch][n][n] row-major, or NULL = S is None for every ego (the reference resets
  *        self.S on every solve, so pass it before each solve);
  *   s_on [batch] (NULL = 1 for all egos when S is given): 0 marks "S is None" for that ego;
  *   bx   [batch][nFx], or NULL = keep the current bound (the reference keeps self.bx).
- * With S on, the state rows are Fx S x <= bx, the cones' middle rows use W1 S
- * (buildIneqConstr :1894-1901,:1935-1937) and, on updates, the collision row's dh[0] is
- * pushed to sign(dh0) max(0.1, |dh0|) while its rhs keeps the unclipped h0 (:2025-2036).
- * mask NULL = all egos. */
+ * The state rows follow the reference's build / update split exactly: the first solve
+ * (buildIneqConstr :1894-1901) writes Fx S x <= bx (Fx x <= bx without S) from the current
+ * Fx and bx; a later solve rewrites them only when S is on (updateIneqConstr :2025-2036), and
+ * then also pushes the collision row's dh[0] to sign(dh0) max(0.1, |dh0|) while its rhs keeps
+ * the unclipped h0; with S off the rows and their bound keep their last values (:2016-2024
+ * patch the collision row alone).  The cones' middle rows use W1 S (W1 without S) on every
+ * solve (:1935-1937, :1995-1998).  mask NULL = all egos. */
 int bmpc_set_transform(bmpc_plan* plan, const double* S, const uint8_t* s_on, const double* bx,
                        const uint8_t* mask);
+/* Per-ego state-constraint matrix Fx [batch][nFx][n] of the next solves: the Fx argument of
+ * BranchMPC_CVaR.solve (self.Fx = Fx, kept until the next one, MPC_branch.py:2055-2056).  It
+ * enters the state rows under the rule of bmpc_set_transform (first solve, or S on).  Same
+ * plans as bmpc_set_transform; the row count must stay nFx.  mask NULL = all egos. */
+int bmpc_set_fx(bmpc_plan* plan, const double* Fx, const uint8_t* mask);
 
 /* Tree of the last solve (host copies; NULL skips):
  *   xbar,zbar [batch][T][n]  ubar [batch][U][d]  w [batch][nbranch]
  *   p [batch][bdim][m]       sol [batch][nv]   (full primal vector, reference layout) */
 int bmpc_get_tree(bmpc_plan* plan, double* xbar, double* ubar, double* zbar, double* w,
                   double* p, double* sol);
+/* dp = d p / d x of every non-leaf branch of the last solve, [batch][bdim][m][n]: the
+ * BranchTree.dp that inittree / updatetree set from branch_eval (MPC_branch.py:1711,1842). */
+int bmpc_get_branch_dp(bmpc_plan* plan, double* dp);
 
 /* Average device time per call of each kernel over the solves since the last call
  * (HIP events on the launch stream); ms[0] = tree/linearisation kernel, ms[1] = IPM

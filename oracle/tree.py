@@ -236,6 +236,7 @@ class CVaRController:
         self.Solution = None
         self.S = None            # state transformation of the current solve (merge scene)
         self._first = True
+        self._rows = self._brows = None   # state rows / bound in force (None: not built yet)
 
     # ---- sizes ---------------------------------------------------------------------
     @property
@@ -308,7 +309,7 @@ class CVaRController:
         hx = np.zeros(t.T * Nc)
         # with a state transformation S (MPC_branch.py:1894-1901, :2025-2036): Fx S rows, and on
         # updates dh[0] <- sign(dh0) max(0.1, |dh0|) in the row while h keeps the unclipped dh
-        FxS = self.Fx if self.S is None else self.Fx @ self.S
+        FxS, bxr = self._rows, self._brows       # the state rows as built / last updated
         for b in range(t.nbranch):
             for j in range(t.length[b]):
                 h0, dh = self.model.col_eval(tr.xtraj[b][j], tr.ztraj[b][j])
@@ -321,7 +322,7 @@ class CVaRController:
                     for c in range(n):
                         if blk[r, c] != 0.0:
                             rows.append(k * Nc + r); cols.append(L['X'] + k * n + c); vals.append(blk[r, c])
-                hx[k * Nc:(k + 1) * Nc] = np.append(h0, self.bx)
+                hx[k * Nc:(k + 1) * Nc] = np.append(h0, bxr)
         for k in range(t.T * Nc):
             rows.append(k); cols.append(L['S'] + k); vals.append(-1.0)
         h.append(hx)
@@ -413,17 +414,25 @@ class CVaRController:
         return G, np.concatenate(h), {'l': n_lp, 'q': qdims}
 
     # ---- solve (:2043-2092) ------------------------------------------------------------
-    def setup_problem(self, x, z, xRef=None, S=None, bx=None):
-        """``solve`` (:2043-2057): xRef kept when None, S reset every solve, bx kept when None."""
+    def setup_problem(self, x, z, xRef=None, S=None, bx=None, Fx=None):
+        """``solve`` (:2043-2057): xRef, Fx and bx kept when None, S reset every solve.  The
+        state rows (Fx S | bx) are written by buildIneqConstr on the first solve (:1894-1901)
+        and by updateIneqConstr only when S is not None (:2025-2036); with S None a later solve
+        keeps the rows it finds (:2016-2024 patch the collision row alone)."""
         x = np.asarray(x, float)
         z = np.asarray(z, float)
         if xRef is not None:
             self.xRef = np.asarray(xRef, float)
         self.S = None if S is None else np.asarray(S, float)
+        if Fx is not None:
+            self.Fx = np.asarray(Fx, float).reshape(-1, self.n)
         if bx is not None:
             self.bx = np.asarray(bx, float).reshape(-1)
         first = self.tree is None
         self._first = first
+        if first or self.S is not None or self._rows is None:   # (a resumed controller builds them)
+            self._rows = self.Fx if self.S is None else self.Fx @ self.S
+            self._brows = self.bx.copy()
         if first:
             self.tree = TreeState(self.topo, self.n, self.d)
             self.Jcons = float(self.xRef @ self.Q @ self.xRef)
@@ -454,8 +463,8 @@ class CVaRController:
         out.append(0.5 * math.log(max(1.0, ub @ self.R @ ub)))
         return out
 
-    def solve(self, x, z, xRef=None, S=None, bx=None):
-        prob = self.setup_problem(x, z, xRef, S, bx)
+    def solve(self, x, z, xRef=None, S=None, bx=None, Fx=None):
+        prob = self.setup_problem(x, z, xRef, S, bx, Fx)
         sol, info = self.solver(prob)
         self.last_info = info
         self.accept(sol, info['exitFlag'])

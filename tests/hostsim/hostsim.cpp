@@ -127,7 +127,9 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   for (int e = 0; e < h->batch; ++e) {
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;
-    if (P.desc.model == BMPC_MODEL_HIGHWAY && lean)
+    if (P.desc.model == BMPC_MODEL_HIGHWAY && (P.desc.flags & BMPC_PLAN_TRANSFORM))
+      r = solve_ego<HostExecT<true>, HighwayT>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY && lean)
       r = solve_ego<HostExecT<false, false>, Highway>(exl, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
     else if (P.desc.model == BMPC_MODEL_HIGHWAY)
       r = solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
@@ -192,6 +194,29 @@ int hs_set_transform(void* p, const double* S, const uint8_t* s_on, const double
       xf[XF_BXSET] = 1.0;
     }
   }
+  return 0;
+}
+
+// bmpc_set_fx of the host build (solve's Fx argument, kept until the next one)
+int hs_set_fx(void* p, const double* Fx) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  for (int e = 0; e < h->batch; ++e) {
+    double* xf = h->ws.data() + L.stride * e + L.xform;
+    for (int i = 0; i < P.nFx * P.n; ++i) xf[XF_FX + i] = Fx[(size_t)e * P.nFx * P.n + i];
+    xf[XF_FXSET] = 1.0;
+  }
+  return 0;
+}
+
+// BranchTree.dp of every non-leaf branch [batch][bdim][m][n] (bmpc_get_branch_dp)
+int hs_get_branch_dp(void* p, double* dp) {
+  HS* h = (HS*)p;
+  const Plan& P = h->hp.plan;
+  const Layout& L = h->hp.lay;
+  const size_t k = (size_t)P.bdim * P.m * P.n;
+  for (int e = 0; e < h->batch; ++e) memcpy(dp + e * k, h->ws.data() + L.stride * e + L.dp, sizeof(double) * k);
   return 0;
 }
 

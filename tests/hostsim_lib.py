@@ -29,12 +29,31 @@ SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", 
 HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")]
 
 
+def source_hash():
+    """Hash of the sources, headers and flag set a host build is compiled from (the sidecar
+    ``<so>.srchash`` records it: an mtime check would accept a stale binary)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(SRCS + HDRS + [os.path.join(REPO, "include", "bmpc.h")]):
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def build(force=False):
-    newest = max(os.path.getmtime(p) for p in SRCS + HDRS + [os.path.join(REPO, "include", "bmpc.h")])
-    if force or not os.path.exists(SO) or os.path.getmtime(SO) < newest:
+    stamp = SO + ".srchash"
+    want = source_hash()
+    have = open(stamp).read().strip() if os.path.exists(stamp) and os.path.exists(SO) else None
+    if force or have != want:
+        tmp = SO + f".{os.getpid()}.tmp"
         cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fopenmp", "-Wno-unknown-pragmas",
-               *FLAGS, "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", SO]
+               *FLAGS, "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", tmp]
         subprocess.check_call(cmd)
+        os.replace(tmp, SO)                      # atomic: concurrent test workers each build their own
+        with open(stamp + f".{os.getpid()}", "w") as f:
+            f.write(want + "\n")
+        os.replace(stamp + f".{os.getpid()}", stamp)
     return SO
 
 
@@ -117,6 +136,17 @@ class HostSim:
         bx = None if bx is None else np.ascontiguousarray(np.asarray(bx, float).reshape(B, self.desc.nFx))
         on = None if s_on is None else np.ascontiguousarray(s_on, np.uint8)
         lib().hs_set_transform(self.h, _p(S), _p(on), _p(bx))
+
+    def set_fx(self, Fx):
+        """Per-ego Fx [B,nFx,n] of the next solves (solve's Fx argument)."""
+        Fx = np.ascontiguousarray(np.asarray(Fx, float).reshape(self.batch, self.desc.nFx, self.desc.n))
+        lib().hs_set_fx(self.h, _p(Fx))
+
+    def branch_dp(self):
+        """BranchTree.dp of every non-leaf branch [B, bdim, m, n] of the last solve."""
+        out = np.zeros((self.batch, self.bdim, self.desc.m, self.desc.n))
+        lib().hs_get_branch_dp(self.h, _p(out))
+        return out
 
     def set_robust_warm_start(self, xlin, ulin, oldu):
         xlin, ulin, oldu = (np.ascontiguousarray(a, dtype=np.float64) for a in (xlin, ulin, oldu))

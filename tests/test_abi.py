@@ -34,7 +34,7 @@ def test_library_is_gfx950_code_object():
 def test_abi_version_without_device():
     from bmpc import _lib
     lib = _lib.load()
-    assert lib.bmpc_abi_version() == 1
+    assert lib.bmpc_abi_version() == 2
 
 
 def test_desc_struct_layout_matches_header():
@@ -43,16 +43,17 @@ def test_desc_struct_layout_matches_header():
     import tempfile
     from bmpc import abi
     code = ('#include <stdio.h>\n#include <stddef.h>\n#include "bmpc.h"\n'
-            'int main(){printf("%zu %zu %zu %zu\\n", sizeof(bmpc_plan_desc), offsetof(bmpc_plan_desc, Q),'
-            ' offsetof(bmpc_plan_desc, mc), sizeof(bmpc_policy));return 0;}\n')
+            'int main(){printf("%zu %zu %zu %zu %zu\\n", sizeof(bmpc_plan_desc), offsetof(bmpc_plan_desc, Q),'
+            ' offsetof(bmpc_plan_desc, mc), sizeof(bmpc_policy), offsetof(bmpc_plan_desc, flags));return 0;}\n')
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
         open(c, "w").write(code)
         exe = os.path.join(d, "t")
         subprocess.check_call(["gcc", "-I" + os.path.join(REPO, "include"), c, "-o", exe])
         out = subprocess.check_output([exe]).decode().split()
-    size, offQ, offmc, psize = map(int, out)
+    size, offQ, offmc, psize, offfl = map(int, out)
     assert size == C.sizeof(abi.PlanDesc)
     assert offQ == abi.PlanDesc.Q.offset
     assert offmc == abi.PlanDesc.mc.offset
     assert psize == C.sizeof(abi.Policy)
+    assert offfl == abi.PlanDesc.flags.offset

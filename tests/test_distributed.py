@@ -29,6 +29,7 @@ def _worker(rank, world, port, total, out):
     stats[D.STAT_J] = float(x[lo:hi, 2].sum())            # stand-in per-ego values
     stats[D.STAT_SOLVES] = hi - lo
     stats[D.STAT_COLL] = float((np.abs(x[lo:hi, 0] - z[lo:hi, 0]) < 4).sum())
+    stats[D.STAT_ANY_COLLIDED] = float(rank == 1)          # a flag only one rank raises
     D.reduce_stats(stats)
     t = D.max_over_ranks(float(rank + 1))
     out[rank] = (stats.numpy().copy(), t, lo, hi)
@@ -51,6 +52,7 @@ def test_two_rank_shard_and_reduce():
     assert s0[D.STAT_SOLVES] == total
     np.testing.assert_allclose(s0[D.STAT_J], x[:, 2].sum(), rtol=1e-12)
     assert s0[D.STAT_COLL] == (np.abs(x[:, 0] - z[:, 0]) < 4).sum()
+    assert s0[D.STAT_ANY_COLLIDED] == 1.0                 # MAX, not the sum over ranks
     assert t0 == t1 == 2.0
 
 
@@ -84,7 +86,8 @@ def _episode(lo, hi, total, steps, N=10, NB=1):
         else:
             x, z, xref = hs.env_step(env, t, scene, r["upred"], r["J"], r["status"], r["iters"], estats)
         r = hs.solve(x, z, xref)
-    return estats.sum(0)
+    from bmpc import distributed as D
+    return D.episode_stats(estats)
 
 
 def _loop_worker(rank, world, port, total, steps, out):

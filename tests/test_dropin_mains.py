@@ -41,6 +41,12 @@ class _HostPlan:
     def set_transform(self, S=None, bx=None, s_on=None, mask=None):
         self._hs.set_transform(S, bx, s_on)
 
+    def set_fx(self, Fx, mask=None):
+        self._hs.set_fx(Fx)
+
+    def branch_dp(self):
+        return self._hs.branch_dp()
+
 
 @pytest.fixture
 def host_device(monkeypatch):

@@ -28,7 +28,7 @@ def gpu():
 
 def test_library_is_native(gpu):
     from bmpc import _lib
-    assert _lib.lib().bmpc_abi_version() == 1
+    assert _lib.lib().bmpc_abi_version() == 2
 
 
 def test_model_eval_matches_oracle(gpu):

@@ -1,0 +1,197 @@
+"""solve's S / Fx / bx arguments on the plain highway model and the live tree's dp.
+
+The fixture ``highway_xform_n8_nb2`` is the reference's own ``BranchMPC_CVaR`` (tools/
+gen_golden.py, ``gen_highway_xform``) in the overtake scene with a schedule of S / Fx / bx
+arguments (``xform_schedule``): S on some steps and None on others, a new Fx and a new bx
+on steps with S off -- where the reference keeps the state rows it built earlier
+(updateIneqConstr, MPC_branch.py:2016-2024) -- and with S on (:2025-2036).  It records every
+step's inputs, exit code, J, uPred[0] and the live tree's ``BranchTree.dp`` (:1711, :1842),
+and the exact solver problems on kept steps.
+
+Replays are sequential (one ego, its own warm start, the recorded inputs), because the state
+rows in force depend on the whole argument history.  Tolerances: assembly 1e-12 (oracle vs
+the reference's matrices); J 1e-6 relative and uPred[0] 1e-6 on steps both sides solve to
+exit 0 (ECOS's 1e-8 certificates bound the difference of two optima, observed <= 1e-7);
+dp of the root branch 1e-12 (it is evaluated at the ego's input state), of the depth-1
+branches 1e-6 (they sit at the end of the warm-started rollout, whose inputs are the previous
+solution, itself known to ~1e-8)."""
+import numpy as np
+import pytest
+
+from common import coo, golden, highway_desc_from_golden, highway_policy_rows
+
+NAME = "highway_xform_n8_nb2"
+
+
+def schedule(g, t):
+    S = g["traj_S"][t] if g["traj_S_on"][t] else None
+    Fx = g["traj_Fx"][t] if g["traj_Fx_on"][t] else None
+    bx = g["traj_bx"][t] if g["traj_bx_on"][t] else None
+    return S, Fx, bx
+
+
+def xform_desc(g):
+    from bmpc import abi
+    d = highway_desc_from_golden(g)
+    d.flags = abi.PLAN_TRANSFORM
+    return d
+
+
+def replay(solver, g, steps):
+    """Drive a HostSim / BatchPlan (batch 1) through the recorded steps with the schedule."""
+    out = dict(status=[], J=[], u0=[], dp=[])
+    last_tgt = None
+    for t in range(steps):
+        tgt = tuple(g["traj_lc_target"][t])
+        if tgt != last_tgt:
+            solver.set_policies(highway_policy_rows([tgt], float(g["Kpsi"])))
+            last_tgt = tgt
+        S, Fx, bx = schedule(g, t)
+        if Fx is not None:
+            solver.set_fx(np.asarray(Fx)[None])
+        solver.set_transform(None if S is None else np.asarray(S)[None], None if bx is None else np.asarray(bx)[None])
+        r = solver.solve(g["traj_x"][t][None], g["traj_z"][t][None], g["traj_xRef"][t][None])
+        out["status"].append(int(r["status"][0]))
+        out["J"].append(float(r["J"][0]))
+        out["u0"].append(r["upred"][0, 0].copy())
+        out["dp"].append(solver.branch_dp()[0].copy())
+    return {k: np.array(v) for k, v in out.items()}
+
+
+def check_replay(out, g, steps):
+    ex = np.asarray(g["traj_exit"][:steps])
+    assert np.all(out["status"] >= 0), out["status"]
+    assert np.mean(out["status"] == ex) >= 0.9, (out["status"], ex)
+    both = (out["status"] == 0) & (ex == 0)
+    Jr = np.asarray(g["traj_J"][:steps])
+    np.testing.assert_allclose(out["J"][both], Jr[both], rtol=1e-6)
+    np.testing.assert_allclose(out["u0"][both], np.asarray(g["traj_u"][:steps])[both], atol=1e-6)
+    dpr = np.asarray(g["traj_dp"][:steps])
+    np.testing.assert_allclose(out["dp"][:, 0], dpr[:, 0], rtol=1e-12, atol=1e-12)   # root branch
+    np.testing.assert_allclose(out["dp"], dpr, atol=1e-6)
+
+
+def test_fixture_exercises_the_schedule():
+    """The recording covers S on / off, Fx and bx changes under both, and a non-zero dp."""
+    g = golden(NAME)
+    on = g["traj_S_on"]
+    assert on.any() and (~on).any()
+    fx_steps = np.flatnonzero(g["traj_Fx_on"])
+    assert any(not on[t] for t in fx_steps)
+    bx_steps = np.flatnonzero(g["traj_bx_on"])
+    assert any(not on[t] for t in bx_steps) and any(on[t] for t in bx_steps)
+    assert np.abs(g["traj_dp"]).max() > 1e-6
+
+
+def test_oracle_restates_reference_rows():
+    """The oracle controller, fed the recorded inputs and the same S / Fx / bx sequence,
+    rebuilds the reference's exact problem on every kept step (sticky rows included) and
+    reaches the same J."""
+    from oracle.ecos_ipm import ecos_solve
+    from oracle.model import HighwayModel, highway_policies
+    from oracle.tree import CVaRController
+    g = golden(NAME)
+    keep = [int(v) for v in g["keep"]]
+    N, NB = int(g["N"]), int(g["NB"])
+    mdl = HighwayModel(N, float(g["dt"]), highway_policies(float(g["Kpsi"]), g["traj_lc_target"][0]),
+                       L=float(g["L"]), W=float(g["W"]), s1=float(g["s1"]))
+    c = CVaRController(mdl, N, NB, g["Q"], g["R"], g["Fx"], g["bx"], g["Fu"], g["bu"], g["Qslack"], g["xRef0"],
+                       float(g["ralpha"]), solver=ecos_solve)
+    topo = c.topo
+    for t in range(max(keep) + 1):
+        mdl.update_backup(highway_policies(float(g["Kpsi"]), g["traj_lc_target"][t]))
+        S, Fx, bx = schedule(g, t)
+        if t in keep and t - 1 in keep:
+            # the warm start the reference carried (its own previous solution): the oracle's
+            # sequential solution differs from it by ~1e-9, which would move dh at that level
+            uP = g[f"s{t - 1}_sol"][topo.T * c.n: topo.T * c.n + topo.U * c.d].reshape(topo.U, c.d)
+            c.uLin = np.vstack((uP, uP[-1]))
+        c.solve(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t], S=S, bx=bx, Fx=Fx)
+        # the problems agree to rounding (the reference's model runs over the CasADi stand-in,
+        # the oracle's in NumPy); the IPM certifies each optimum to 1e-8, so J agrees to ~1e-9
+        assert abs(c.last_info["x"][-1] - g["traj_J"][t]) <= 1e-7 * abs(g["traj_J"][t]), t
+        np.testing.assert_allclose(c.tree.dp[0], g["traj_dp"][t][0], rtol=1e-12, atol=1e-12)
+        if t in keep and (t == 0 or t - 1 in keep):
+            prob, p = c.last_problem, f"s{t}_"
+            for mine, key in ((prob.G, "G"), (prob.A, "A")):
+                ref = coo(g, p + key)
+                assert abs(mine - ref).max() <= 1e-12 * max(1.0, abs(ref).max()), (t, key)
+            np.testing.assert_allclose(prob.h, g[p + "h"], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(prob.b, g[p + "b"], rtol=1e-12, atol=1e-12)
+
+
+def test_host_build_replays_xform_scene():
+    """The kernel templates (host build) replay the whole recording."""
+    import hostsim_lib as H
+    g = golden(NAME)
+    steps = len(g["traj_x"])
+    hs = H.HostSim(xform_desc(g), 1)
+    check_replay(replay(hs, g, steps), g, steps)
+
+
+def test_host_build_sticky_rows_matter():
+    """Sanity of the fixture: applying Fx / bx on the steps with S off (instead of keeping the
+    rows, as the reference does) changes the solution -- so the replay above tests the rule."""
+    import hostsim_lib as H
+    g = golden(NAME)
+    t_fx = int(next(t for t in np.flatnonzero(g["traj_Fx_on"]) if not g["traj_S_on"][t]))
+    steps = t_fx + 1
+    hs = H.HostSim(xform_desc(g), 1)
+    keep = replay(hs, g, steps)
+    hs2 = H.HostSim(xform_desc(g), 1)
+    out = dict(J=[])
+    for t in range(steps):
+        hs2.set_policies(highway_policy_rows([g["traj_lc_target"][t]], float(g["Kpsi"])))
+        S, Fx, bx = schedule(g, t)
+        if Fx is not None:
+            hs2.set_fx(np.asarray(Fx)[None])
+        # force the rows to be rewritten every step: an explicit identity S does that
+        hs2.set_transform(np.eye(4)[None] if S is None else np.asarray(S)[None],
+                          None if bx is None else np.asarray(bx)[None])
+        out["J"].append(hs2.solve(g["traj_x"][t][None], g["traj_z"][t][None], g["traj_xRef"][t][None])["J"][0])
+    assert abs(out["J"][-1] - keep["J"][-1]) > 1e-6 * abs(keep["J"][-1])
+
+
+@pytest.mark.gpu
+def test_gpu_replays_xform_scene():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from bmpc import plan
+    g = golden(NAME)
+    steps = len(g["traj_x"])
+    pl = plan.BatchPlan(xform_desc(g), 1)
+    check_replay(replay(pl, g, steps), g, steps)
+
+
+@pytest.mark.gpu
+def test_gpu_compat_controller_takes_fx_and_s():
+    """The drop-in BranchMPC_CVaR.solve(x, z, xRef, S, Fx, bx) on the highway model, with
+    BranchTree.dp on the live tree, against the same recording."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import Init_MPC
+    import MPC_branch
+    from highway_branch_dyn import PredictiveModel, backup_brake, backup_lc, backup_maintain
+    from utils import Branch_constants
+    g = golden(NAME)
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=6.0, rm=0.3, J_c=20, s_c=1,
+                            ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    N, NB = int(g["N"]), int(g["NB"])
+    steps = 10
+    tg = g["traj_lc_target"]
+    model = PredictiveModel(4, 2, N, [lambda x: backup_maintain(x, cons), lambda x: backup_brake(x, cons),
+                                      lambda x: backup_lc(x, tg[0])], 0.1, cons)
+    mpc = MPC_branch.BranchMPC_CVaR(Init_MPC.initBranchMPC(4, 2, N, NB, g["xRef0"], 6.0, 0.3, 4, cons.W), model, 0.9)
+    for t in range(steps):
+        if t > 0 and np.any(tg[t] != tg[t - 1]):
+            model.update_backup([lambda x: backup_maintain(x, cons), lambda x: backup_brake(x, cons),
+                                 lambda x, tt=tg[t]: backup_lc(x, tt)])
+        S, Fx, bx = schedule(g, t)
+        mpc.solve(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t], S=S, Fx=Fx, bx=bx)
+        if mpc.status == 0 and g["traj_exit"][t] == 0:
+            assert abs(mpc.J - g["traj_J"][t]) <= 1e-6 * abs(g["traj_J"][t]), t
+            np.testing.assert_allclose(mpc.uPred[0], g["traj_u"][t], atol=1e-6)
+        np.testing.assert_allclose(mpc.BT.dp, g["traj_dp"][t][0], rtol=1e-12, atol=1e-12)
+        assert mpc.BT.children[0].dp.shape == (3, 4)

@@ -230,6 +230,100 @@ def gen_highway(name, N, NB, steps, keep, out):
     np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
 
 
+# solve's S / Fx / bx schedule of the transform fixture (MPC_branch.py:2043-2057): S on some
+# steps and None on others, a new Fx and a new bx on steps with S off (the reference keeps the
+# state rows then: updateIneqConstr :2016-2024) and with S on (:2025-2036)
+XF_S1 = np.array([[1.0, 0.0, 0.0, 0.0], [0.0, 1.0, 0.01, 0.0], [0.0, 0.0, 1.0, 0.0], [0.0, 0.0, 0.0, 1.0]])
+XF_S2 = np.array([[1.0, 0.0, 0.0, 0.0], [0.0, 0.98, 0.0, 0.0], [0.0, 0.0, 1.0, 0.0], [0.0, 0.0, 0.05, 1.0]])
+XF_FX2 = np.diag([1.0, 1.0, 2.0, 2.0]) @ np.array([[0., 1, 0, 0], [0, -1, 0, 0], [0, 0, 0, 1], [0, 0, 0, -1]])
+
+
+def xform_schedule(t):
+    """(S, Fx, bx) passed to solve at step t (None = argument omitted)."""
+    S = {1: XF_S1, 6: XF_S2, 8: np.eye(4), 9: XF_S1, 12: XF_S2, 13: XF_S2, 16: np.eye(4)}.get(t)
+    Fx = XF_FX2 if t in (5, 14) else None
+    bx = {7: [4 * 3.6 - 1.0, -1.0, 0.2, 0.2], 13: [4 * 3.6 - 1.25, -1.25, 0.25, 0.25]}.get(t)
+    return S, Fx, bx
+
+
+class XformProxy:
+    """The controller as the overtake env sees it, passing the schedule's S / Fx / bx."""
+
+    def __init__(self, mpc):
+        self.mpc, self.t = mpc, 0
+
+    def solve(self, x, z, xRef):
+        S, Fx, bx = xform_schedule(self.t)
+        self.mpc.solve(x, z, xRef, S=S, Fx=Fx, bx=bx)
+        self.t += 1
+
+    def __getattr__(self, k):
+        return getattr(self.mpc, k)
+
+
+def gen_highway_xform(name, N, NB, steps, keep, out):
+    """The overtake scene with solve's S / Fx / bx arguments (xform_schedule) and the live
+    tree's dp recorded every step: the reference's own BranchMPC_CVaR under its build / update
+    rules for the state rows."""
+    import Init_MPC
+    import MPC_branch
+    from utils import Branch_constants
+
+    n, d, dt, am, rm, N_lane = 4, 2, 0.1, 6.0, 0.3, 4
+    xRef0 = np.array([0.5, 1.8, 15, 0])
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=am, rm=rm, J_c=20,
+                            s_c=1, ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    model = RefHighwayModel(N, dt, cons, xRef0)
+    param = Init_MPC.initBranchMPC(n, d, N, NB, xRef0, am, rm, N_lane, cons.W)
+    mpc = MPC_branch.BranchMPC_CVaR(param, model, ralpha=0.9)
+    CURRENT["mpc"] = mpc
+    env = HighwayOvertake(XformProxy(mpc), model, N_lane=N_lane, L=cons.L, W=cons.W, Kpsi=cons.Kpsi,
+                          lc_target0=xRef0, dt=dt)
+    d_out = dict(N=N, NB=NB, m=3, n=n, d=d, dt=dt, am=am, rm=rm, N_lane=N_lane, ralpha=0.9,
+                 L=cons.L, W=cons.W, Kpsi=cons.Kpsi, s1=cons.s1, xRef0=xRef0,
+                 Q=param.Q, R=param.R, Fx=param.Fx, bx=np.asarray(param.bx, float).reshape(-1),
+                 Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
+    traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "exit", "J", "iters", "S", "S_on", "Fx", "Fx_on",
+                            "bx", "bx_on", "dp")}
+    t0 = time.time()
+    for t in range(steps):
+        if not env.collision:
+            env.check_collision()
+        S, Fx, bx = xform_schedule(t)
+        r = env.step(t)
+        prob, sol, info, kw = CURRENT["captured"]
+        for k in ("x", "z", "xRef", "u", "lc_target"):
+            traj[k].append(r[k])
+        traj["exit"].append(info["exitFlag"])
+        traj["J"].append(sol[-1])
+        traj["iters"].append(info["iter"])
+        traj["S"].append(np.eye(n) if S is None else np.asarray(S, float))
+        traj["S_on"].append(S is not None)
+        traj["Fx"].append(np.zeros((4, n)) if Fx is None else np.asarray(Fx, float))
+        traj["Fx_on"].append(Fx is not None)
+        traj["bx"].append(np.zeros(4) if bx is None else np.asarray(bx, float))
+        traj["bx_on"].append(bx is not None)
+        traj["dp"].append(np.array([np.asarray(b.dp, float) for b in mpc.ndx if b.depth < NB]))
+        if t in keep:
+            p = f"s{t}_"
+            coo(prob.G, p + "G", d_out)
+            coo(prob.A, p + "A", d_out)
+            d_out[p + "c"] = prob.c
+            d_out[p + "h"] = prob.h
+            d_out[p + "b"] = prob.b
+            d_out[p + "dims_l"] = np.array(prob.dims["l"])
+            d_out[p + "dims_q"] = np.array(prob.dims["q"])
+            d_out[p + "cone_boost"] = np.array(prob.cone_boost)
+            d_out[p + "sol"] = sol
+            d_out[p + "exit"] = np.array(info["exitFlag"])
+        print(f"[{name}] t={t:3d} exit={info['exitFlag']:3d} it={info['iter']:3d} J={sol[-1]:.6f} "
+              f"u0={mpc.uPred[0]} ({time.time() - t0:.0f}s)", flush=True)
+    for k, v in traj.items():
+        d_out["traj_" + k] = np.array(v)
+    d_out["keep"] = np.array(sorted(keep))
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **d_out)
+
+
 def gen_highway_qp(name, N, NB, steps, keep, out):
     """main_branch.py's overtake scene with the (commented-out) ``BranchMPC`` controller
     (main_branch.py:46; the active class definition is MPC_branch.py:881)."""
@@ -663,7 +757,9 @@ def main():
         "highway_n20_nb1": lambda: gen_highway("highway_n20_nb1", 20, 1, 8 if a.quick else 100, {0, 1, 2, 5, 50}, out),
         "highway_n8_nb2": lambda: gen_highway("highway_n8_nb2", 8, 2, 5 if a.quick else 40, {0, 1, 2, 30}, out),
         "highway_n10_nb1": lambda: gen_highway("highway_n10_nb1", 10, 1, 5 if a.quick else 20, {0, 1}, out),
-        "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 2, {0, 1}, out),
+        "highway_n30_nb2": lambda: gen_highway("highway_n30_nb2", 30, 2, 3 if a.quick else 24, {0, 1, 12}, out),
+        "highway_xform_n8_nb2": lambda: gen_highway_xform("highway_xform_n8_nb2", 8, 2, 5 if a.quick else 18,
+                                                          {0, 1, 2, 5, 6, 7, 8}, out),
         "highway_qp_n8_nb2": lambda: gen_highway_qp("highway_qp_n8_nb2", 8, 2, 5 if a.quick else 30, {0, 1, 2, 15}, out),
         "highway_robust_n20_nb1": lambda: gen_highway_robust("highway_robust_n20_nb1", 20, 1, 5 if a.quick else 30, {0, 1, 2, 15}, out),
         "highway_robust_n8_nb2": lambda: gen_highway_robust("highway_robust_n8_nb2", 8, 2, 5 if a.quick else 20, {0, 1, 10}, out),
