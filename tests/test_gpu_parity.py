@@ -54,7 +54,7 @@ def test_model_eval_matches_oracle(gpu):
 
 
 @pytest.mark.parametrize("name,steps", [("highway_n20_nb1", 100), ("highway_n8_nb2", 40), ("highway_n10_nb1", 20),
-                                        ("highway_n30_nb2", 2)])
+                                        ("highway_n30_nb2", 24)])
 def test_replay_matches_reference(gpu, name, steps):
     """Every step of the reference's recorded closed loop, one ego per step, each with the
     warm start the reference carried into it (set through the checkpoint ABI), in ONE

@@ -49,7 +49,7 @@ def _T(g):
 
 
 @pytest.mark.parametrize("name,steps", [("highway_n10_nb1", 20), ("highway_n8_nb2", 40), ("highway_n20_nb1", 100),
-                                        ("highway_n30_nb2", 2)])
+                                        ("highway_n30_nb2", 24)])
 def test_host_build_replays_reference(name, steps):
     g = golden(name)
     rb = replay_batch(g, steps)
