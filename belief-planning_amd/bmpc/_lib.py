@@ -16,6 +16,7 @@ INCLUDE = os.path.join(REPO, "include")
 SO_PATH = os.path.join(PKG_DIR, "libbmpc.so")
 PROF_SO_PATH = os.path.join(PKG_DIR, "libbmpc_prof.so")   # -DBMPC_PROFILE variant (tools only)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+EXTRA_FLAGS = []      # experiment builds (tools/build_variant.py) append -D flags here
 ARCH = os.environ.get("BMPC_OFFLOAD_ARCH", "gfx950")
 
 
@@ -24,7 +25,11 @@ class BmpcUnavailable(RuntimeError):
 
 
 def sources():
-    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_plan.cpp", "bmpc_qpplan.cpp")]
+    """Translation units of libbmpc.so: the C ABI + small kernels, one unit per predictive model's
+    solver kernels (compiled in parallel), the host-side plan builders."""
+    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_k_highway.hip", "bmpc_k_highway_t.hip",
+                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_plan.cpp",
+                                            "bmpc_qpplan.cpp")]
 
 
 def headers():
@@ -44,13 +49,25 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False) -> 
         with open(stamp) as f:
             if f.read().strip() == want:
                 return out
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
-           *(["-DBMPC_PROFILE"] if profile else []),
-           "-I" + INCLUDE, "-I" + CSRC, *sources(), "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
+             *(["-DBMPC_PROFILE"] if profile else []), *EXTRA_FLAGS, "-I" + INCLUDE, "-I" + CSRC]
+    with tempfile.TemporaryDirectory(prefix="bmpc_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in sources()]
+        cmds = [[HIPCC, *flags, "-c", src, "-o", obj] for src, obj in zip(sources(), objs)]
+        if verbose:
+            for c in cmds:
+                print(" ".join(c))
+        jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(cmds), os.cpu_count() or 1)
+        with ThreadPoolExecutor(jobs) as pool:
+            for f in [pool.submit(subprocess.check_call, c) for c in cmds]:
+                f.result()
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+        if verbose:
+            print(" ".join(link))
+        subprocess.check_call(link)
     os.replace(out + ".tmp", out)
     with open(stamp, "w") as f:
         f.write(want + "\n")

@@ -129,6 +129,7 @@ struct Plan {
   int nsm;    // dense coupling system size
   // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
   int lds_M, lds_piv, lds_rhs, lds_red, nlds;
+  int lds_w;  // W1 (n x n) then Wu (d x d): read with lane-varying rows (apply_G's cone rows)
   int nlds_lean;            // LDS doubles when the coupling system lives in the slab (Layout::coup)
   int lds_scr, nscr;       // tree-solve LDS scratch (slack terms of the pre-pass; 0 = none)
   int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
@@ -276,7 +277,11 @@ BMPC_HD void lane_batch(const X& ex, int lo, int hi, Ld ld, St st) {
 }
 
 // per-lane partial reduction of f(i) over first, first+stride, ... < hi with UN
-// independent accumulators (op: 0 sum, 1 max, 2 min)
+// independent accumulators (op: 0 sum, 1 max, 2 min).  The slots past hi are masked by
+// arithmetic, not by a select on f's value: the compiler turns a select whose operand is a
+// load (or a division) into a branch around it, i.e. one memory round trip per element.
+// For finite values the result is bit-identical (x + 0*v == x; fmax / fmin ignore the NaN of
+// v + (-inf) or v + inf).
 template <int UN = 8, int OP = 0, class F>
 BMPC_HD double strided_partial(int first, int stride, int hi, F f) {
   const double init = OP == 0 ? 0.0 : OP == 1 ? -1e300 : 1e300;
@@ -287,9 +292,11 @@ BMPC_HD double strided_partial(int first, int stride, int hi, F f) {
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int i = b + u * stride;
-      const double v = f(i < hi ? i : b);   // unconditional (see strided_batch)
-      const double r = OP == 0 ? acc[u] + v : OP == 1 ? fmax(acc[u], v) : fmin(acc[u], v);
-      acc[u] = i < hi ? r : acc[u];
+      const bool in = i < hi;
+      const double v = f(in ? i : b);   // unconditional (see strided_batch)
+      if constexpr (OP == 0) acc[u] += (in ? 1.0 : 0.0) * v;
+      else if constexpr (OP == 1) acc[u] = fmax(acc[u], v + (in ? 0.0 : -INFINITY));
+      else acc[u] = fmin(acc[u], v + (in ? 0.0 : INFINITY));
     }
   }
   double s = init;

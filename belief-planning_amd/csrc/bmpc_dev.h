@@ -1,0 +1,256 @@
+// bmpc_dev.h -- the solver kernels of libbmpc.so (gfx950) and their launchers.
+//
+// Mapping: one 64-lane wavefront (one 64-thread workgroup) per ego.  k_tree rebuilds the ego's
+// scenario tree (warm start, rollouts, linearisation, collision rows); k_ipm / k_qp run the
+// structured interior-point solve and unpack the solution.  All per-ego state lives in one
+// contiguous slab of HBM (Layout), so every strided lane loop reads and writes contiguous
+// 512-byte segments.  Each predictive model's kernels are instantiated in a translation unit of
+// their own (bmpc_k_*.hip, compiled in parallel); bmpc_hip.hip holds the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "bmpc_env.h"
+#include "bmpc_hmm.h"
+#include "bmpc_plan.h"
+#include "bmpc_qp.h"
+#include "bmpc_qpplan.h"
+#include "bmpc_solve.h"
+
+namespace bmpc {
+namespace dev {
+
+#ifndef BMPC_WPE
+#define BMPC_WPE 4   // waves per SIMD the IPM kernel is register-limited to (4 = all 4096 egos resident)
+#endif
+
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <bool TR, bool TL = true>
+struct DevExecT {
+  static constexpr bool kTransform = TR;   // per-ego S / bx constants in LDS (merge plans)
+  // LDS-rich launch (TL): topology tables copied to LDS and the coupling system in LDS;
+  // lean launch: tables read from the plan's blob, coupling system in the slab
+  static constexpr bool kCoupLds = TL;
+  using tab_ptr = typename std::conditional<TL, lint*, gint*>::type;
+  int lane;
+  ldouble* lds;  // this wave's LDS scratch (Plan::nlds doubles; k_ipm / k_qp only)
+  tab_ptr tab;   // topology tables (k_ipm / k_qp only)
+  ldouble* eco;  // per-ego constants of the solve (ECO_*; kTransform only)
+  static constexpr int nlanes = 64;
+  // task groups of 4 lanes (one DPP quad) for the tree sweeps
+  static constexpr int kTaskLanes = 4;
+  // cone rows per lane the fused IPM passes hold in registers (bmpc_ipm.h, cone_regs)
+  static constexpr int kConeRegRows = 8;
+  __device__ double tsum(double v) const {
+    v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+    return v;
+  }
+  template <int S>
+  __device__ double tget(double v) const { return dpp_d<S | (S << 2) | (S << 4) | (S << 6)>(v); }
+  // sum over aligned groups of g lanes (g a power of two)
+  __device__ double gsum(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ double gmax(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ double gmin(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ void sync() const { __syncthreads(); }
+  // a wave-uniform flag as a scalar: branches on it (and the calls they guard) run with the
+  // full exec mask instead of an exec mask derived from a VGPR the compiler cannot prove uniform
+  __device__ bool uniform(bool b) const { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
+  __device__ double sum(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ double max(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ double min(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+};
+
+using DevExec = DevExecT<false>;
+
+struct Bundle {
+  Plan P;
+  Layout L;
+};
+
+// Dynamic LDS of the solver kernels: Plan::nlds doubles of scratch, then a copy of the
+// topology tables (Plan::ntab int32).  The copy is one batched pass at kernel start; every
+// later tree / cone / node-index lookup of the solve is an LDS read.
+// Dynamic LDS of the solver kernels: Plan::nlds doubles of scratch, then a copy of the
+// topology tables (Plan::ntab int32), then (transform-capable models) ECO_COUNT doubles of
+// per-ego constants.  The table copy is one batched pass at kernel start; every later tree /
+// cone / node-index lookup of the solve is an LDS read.
+__host__ __device__ inline size_t solver_lds_bytes(const Plan& P, bool transform, bool rich) {
+  const size_t tab = rich ? (sizeof(int32_t) * (size_t)P.ntab + 7) & ~(size_t)7 : 0;
+  return sizeof(double) * (size_t)(rich ? P.nlds : P.nlds_lean) + tab + (transform ? sizeof(double) * ECO_COUNT : 0);
+}
+template <bool TR, bool TL>
+__device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* lds_dyn) {
+  const int32_t* gtab = (const int32_t*)P.t.br_depth;   // blob base (the first table)
+  double* eco = lds_dyn + (solver_lds_bytes(P, false, TL) / sizeof(double));
+  // W1 | Wu for the cone passes' per-lane row lookups
+  const int nw = P.n * P.n, nwu = P.d * P.d;
+  for (int i = threadIdx.x; i < nw + nwu; i += 64) lds_dyn[P.lds_w + i] = i < nw ? P.W1[i] : P.Wu[i - nw];
+  if constexpr (TL) {
+    int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
+    for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];
+    __syncthreads();
+    return DevExecT<TR, TL>{(int)threadIdx.x, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco};
+  } else {
+    __syncthreads();
+    return DevExecT<TR, TL>{(int)threadIdx.x, (ldouble*)lds_dyn, (gint*)gtab, (ldouble*)eco};
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
+                                             const bmpc_policy* __restrict__ pol,
+                                             const double* __restrict__ x, const double* __restrict__ z,
+                                             const double* __restrict__ xref, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  DevExec ex{(int)threadIdx.x, nullptr, nullptr, nullptr};
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  BMPC_PROF(E.ws, L, PROF_TREE);
+  tree_step<DevExec, M>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+}
+
+template <class M, bool TL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm(const Bundle* __restrict__ B, double* __restrict__ ws,
+                                            const bmpc_policy* __restrict__ pol, double* upred,
+                                            double* xpred, double* bw, double* J, int32_t* status,
+                                            int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  extern __shared__ double lds_dyn[];
+  const auto ex = solver_exec<M::kTransform, TL>(P, lds_dyn);
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r = solve_ego_ipm<DevExecT<M::kTransform, TL>, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += 64) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += 64) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += 64) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = w[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+}
+
+template <class M, bool TL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_qp(
+    const Bundle* __restrict__ B, double* __restrict__ ws, const bmpc_policy* __restrict__ pol, double* upred,
+    double* xpred, double* bw, double* J, int32_t* status, int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  extern __shared__ double lds_dyn[];
+  const auto ex = solver_exec<false, TL>(P, lds_dyn);
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r = solve_ego_qp<DevExecT<false, TL>, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += 64) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += 64) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += 64) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = r.pcost;
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+}
+
+// one solve launch of a plan (device pointers; the timing events are recorded by the caller
+// between the two launches)
+struct SolveLaunch {
+  const Bundle* bundle;
+  double* ws;
+  const bmpc_policy* pol;
+  const double *x, *z, *xref;
+  double *upred, *xpred, *bw, *J;
+  int32_t *status, *iters;
+  int batch;
+  size_t lds_bytes;   // dynamic LDS of the solver kernel (solver_lds_bytes)
+  bool rich;          // LDS-rich solver launch (choose_lds_rich)
+  bool qp;            // OSQP-class controller (k_qp) instead of the CVaR IPM (k_ipm)
+  hipStream_t stream;
+};
+
+template <class M>
+hipError_t launch_tree(const SolveLaunch& a) {
+  hipLaunchKernelGGL(k_tree<M>, dim3(a.batch), dim3(64), 0, a.stream, a.bundle, a.ws, a.pol, a.x, a.z, a.xref,
+                     a.batch);
+  return hipGetLastError();
+}
+
+template <class K>
+hipError_t launch_solver_kernel(K kernel, const SolveLaunch& a) {
+  if (a.lds_bytes > 64 * 1024) {   // dynamic LDS above 64 KB needs the per-kernel opt-in
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kernel, dim3(a.batch), dim3(64), a.lds_bytes, a.stream, a.bundle, a.ws, a.pol, a.upred,
+                     a.xpred, a.bw, a.J, a.status, a.iters, a.batch);
+  return hipGetLastError();
+}
+
+// WITH_QP: the model also serves the OSQP-class controllers (Prox, BranchMPC, robustMPC)
+template <class M, bool WITH_QP>
+hipError_t launch_solver(const SolveLaunch& a) {
+  if constexpr (WITH_QP) {
+    if (a.qp) return a.rich ? launch_solver_kernel(k_qp<M, true>, a) : launch_solver_kernel(k_qp<M, false>, a);
+  }
+  return a.rich ? launch_solver_kernel(k_ipm<M, true>, a) : launch_solver_kernel(k_ipm<M, false>, a);
+}
+
+// the per-model launchers (bmpc_k_highway.hip, bmpc_k_highway_t.hip, bmpc_k_merge.hip,
+// bmpc_k_quadruped.hip)
+hipError_t launch_tree_highway(const SolveLaunch& a);
+hipError_t launch_solver_highway(const SolveLaunch& a);
+hipError_t launch_tree_highway_t(const SolveLaunch& a);
+hipError_t launch_solver_highway_t(const SolveLaunch& a);
+hipError_t launch_tree_merge(const SolveLaunch& a);
+hipError_t launch_solver_merge(const SolveLaunch& a);
+hipError_t launch_tree_quadruped(const SolveLaunch& a);
+hipError_t launch_solver_quadruped(const SolveLaunch& a);
+
+}  // namespace dev
+}  // namespace bmpc

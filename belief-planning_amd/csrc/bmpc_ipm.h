@@ -155,16 +155,30 @@ BMPC_HD double cone_dot(const X ex, const ConeGroups& G, const gdouble* a, const
 // v0^2 - ||v1||^2 without squaring the dominant entry (see oracle.ecos_ipm.cone_res)
 template <class X>
 BMPC_HD double cone_res(const X ex, const ConeGroups& G, const gdouble* v, int off, int q) {
+  // a lane's largest |v_i| (first index on ties) over batches of 8 loads in flight together
+  constexpr int UN = 8;
   double amax = 0.0, aidx = 1e300;
-  for (int i = 1 + G.gl; i < q; i += G.cg) {
-    const double a = fabs(v[off + i]);
-    if (a > amax) amax = a, aidx = (double)i;
+  for (int b = 1 + G.gl; b < q; b += UN * G.cg) {
+    double a[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int i = b + u * G.cg;
+      a[u] = fabs(v[off + (i < q ? i : b)]);
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int i = b + u * G.cg;
+      const bool take = i < q && a[u] > amax;
+      amax = take ? a[u] : amax;
+      aidx = take ? (double)i : aidx;
+    }
   }
   const double gm = ex.gmax(amax, G.cg);
   const double kd = ex.gmin(amax == gm && aidx < 1e300 ? aidx : 1e300, G.cg);
   const int kidx = kd < 1e300 ? (int)kd : -1;
   const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
-    return i == kidx ? 0.0 : v[off + i] * v[off + i];
+    const double t = v[off + i];
+    return (i == kidx ? 0.0 : 1.0) * (t * t);
   }), G.cg);
   return q > 0 ? cone_res_parts(v[off], gm, ss) : 1.0;
 }
@@ -214,10 +228,10 @@ BMPC_HD void cone_W_regs(const X& ex, const ConeGroups& G, const double (&a)[UC]
 template <int UC, class X>
 BMPC_HD void cone_a_regs(const ConeGroups& G, const gdouble* a, bool jconj, int off, int q, double (&av)[UC]) {
 #pragma unroll
-  for (int uu = 0; uu < UC; ++uu) {
+  for (int uu = 0; uu < UC; ++uu) {   // masked by arithmetic (a select on t would branch around its load)
     const int i = G.gl + uu * G.cg;
     const double t = a[off + (i < q ? i : 0)];
-    av[uu] = i < q ? ((jconj && i > 0) ? -t : t) : 0.0;
+    av[uu] = (i < q ? ((jconj && i > 0) ? -1.0 : 1.0) : 0.0) * t;
   }
 }
 
@@ -317,11 +331,21 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       // the root cone (c < 0) holds the root node's slacks only (ndx = br_ndx[0] = 0)
       const int nn = c >= 0 ? P.N : (k >= 0 ? 1 : 0);
       const double xon = c >= 0 ? -2.0 : 0.0;
-      double part = strided_partial<4>(G.gl, G.cg, nn, [&](int j) {
+      const int Nc = P.Nc;
+      // branch-free: a node's x and slack loads are issued together (the slack loop runs to the
+      // compile-time bound with clamped indices; rows past Nc are multiplied by 0)
+      double part = strided_partial<2>(G.gl, G.cg, nn, [&](int j) {
+        const int xb = P.oX + (ndx + j) * NX, sb = P.oS + (ndx + j) * Nc;
+        double xs[NX], ss[BMPC_MAX_FX + 1];
+#pragma unroll
+        for (int r2 = 0; r2 < NX; ++r2) xs[r2] = zv[xb + r2];
+#pragma unroll
+        for (int cc = 0; cc <= BMPC_MAX_FX; ++cc) ss[cc] = zv[sb + (cc < Nc ? cc : 0)];
         double a = 0.0;
 #pragma unroll
-        for (int r2 = 0; r2 < NX; ++r2) a += xon * qx[r2] * zv[P.oX + (ndx + j) * NX + r2];
-        for (int cc = 0; cc < P.Nc; ++cc) a += Qs * zv[P.oS + (ndx + j) * P.Nc + cc];
+        for (int r2 = 0; r2 < NX; ++r2) a += xon * qx[r2] * xs[r2];
+#pragma unroll
+        for (int cc = 0; cc <= BMPC_MAX_FX; ++cc) a += (cc < Nc ? Qs : 0.0) * ss[cc];
         return a;
       });
       // risk-variable terms, loaded before the reduction and added after it
@@ -339,24 +363,39 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       if (c >= 0 && hasch) acc += rho_c;
       f = acc * ebst;   // exact on the group's lane 0
     }
-    // middle rows: rows are contiguous after each cone's first
+    // middle rows: rows are contiguous after each cone's first: N x-rows blocks (-2 W1 x_j),
+    // then N (root cone: 1) u-row blocks (-2 Wu u_j).  Branch-free: every row loads NX
+    // entries from its node's block (u rows read past their NU entries into valid slab memory
+    // and weight them 0), and the weight row comes from register copies of W1 / Wu, so all
+    // loads of a batch of rows are in flight together.
     const int nxn = c >= 0 ? P.N * NX : 0;
     const int nmid = k < 0 ? 0 : c >= 0 ? P.N * (NX + NU) : NU;
+    // the weight rows come from LDS (a lane-varying row index into registers would become an
+    // indexed private array, i.e. scratch memory): W1 S of this ego or the plan's W1, and Wu
+    const ldouble* W1l = X::kTransform ? ex.eco + ECO_W1 : ex.lds + P.lds_w;
+    const ldouble* Wul = ex.lds + P.lds_w + NX * NX;
+    auto mid_base = [&](int it) {
+      const bool isx = it < nxn;
+      const int iu = isx ? 0 : it - nxn;
+      return isx ? P.oX + (ndx + it / NX) * NX : P.oU + (c >= 0 ? ndu + iu / NU : 0) * NU;
+    };
+    auto mid_val = [&](int it, const double (&zs)[NX]) {
+      const bool isx = it < nxn;
+      const int r = isx ? it % NX : (it - nxn) % NU;
+      const int rx = isx ? r : 0, ru = isx ? 0 : r;
+      double vx = 0.0, vu = 0.0;
+#pragma unroll
+      for (int s2 = 0; s2 < NX; ++s2) vx += -2.0 * W1l[rx * NX + s2] * zs[s2];
+#pragma unroll
+      for (int s2 = 0; s2 < NU; ++s2) vu += -2.0 * Wul[ru * NU + s2] * zs[s2];
+      return isx ? vx : vu;
+    };
     auto mid = [&](int it) {
-      double v = 0.0;
-      if (it < nxn) {
-        const int j = it / NX, r = it % NX;
-        const int xk = ndx + j;
+      const int b = mid_base(it);
+      double zs[NX];
 #pragma unroll
-        for (int s2 = 0; s2 < NX; ++s2) v += -2.0 * w1v(P, ex, r, s2) * zv[P.oX + xk * NX + s2];
-      } else {
-        const int jj = it - nxn;
-        const int j = jj / NU, r = jj % NU;
-        const int uk = c >= 0 ? ndu + j : 0;
-#pragma unroll
-        for (int s2 = 0; s2 < NU; ++s2) v += -2.0 * P.Wu[r * NU + s2] * zv[P.oU + uk * NU + s2];
-      }
-      return v;
+      for (int s2 = 0; s2 < NX; ++s2) zs[s2] = zv[b + s2];
+      return mid_val(it, zs);
     };
     if constexpr (WM == 0) {
       if (k >= 0 && G.gl == 0) {
@@ -368,12 +407,23 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
       // the cone's rows of G zv in registers (q = nmid + 2), then W^-1 (and again for WM = 2)
       const double f0 = ex.gsum(G.gl == 0 ? f : 0.0, G.cg);
       double v[UC], a[UC], y[UC];
+      // the rows' loads in two batches of UC/2 rows (all of a batch in flight together)
 #pragma unroll
-      for (int uu = 0; uu < UC; ++uu) {
-        const int i = G.gl + uu * G.cg;
-        const int im = i >= 1 && i <= nmid ? i - 1 : 0;
-        const double m = mid(im);
-        v[uu] = i >= q ? 0.0 : i == 0 ? f0 : i == q - 1 ? -f0 : m;
+      for (int h = 0; h < UC; h += UC / 2) {
+        double zs[UC / 2][NX];
+#pragma unroll
+        for (int u2 = 0; u2 < UC / 2; ++u2) {
+          const int i = G.gl + (h + u2) * G.cg;
+          const int b = mid_base(i >= 1 && i <= nmid ? i - 1 : 0);
+#pragma unroll
+          for (int s2 = 0; s2 < NX; ++s2) zs[u2][s2] = zv[b + s2];
+        }
+#pragma unroll
+        for (int u2 = 0; u2 < UC / 2; ++u2) {
+          const int i = G.gl + (h + u2) * G.cg;
+          const double m = mid_val(i >= 1 && i <= nmid ? i - 1 : 0, zs[u2]);
+          v[h + u2] = i >= q ? 0.0 : i == 0 ? f0 : i == q - 1 ? -f0 : m;
+        }
       }
       cone_a_regs<UC, X>(G, vn, true, off, q, a);
       const double sc = 1.0 / (k >= 0 ? eta[kk] : 1.0);
@@ -381,7 +431,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
         const int i = G.gl + uu * G.cg;
-        if (WM != 3) y[uu] = i < q ? y[uu] - r3h[off + i] : 0.0;
+        if (WM != 3) y[uu] = (i < q ? 1.0 : 0.0) * (y[uu] - r3h[off + (i < q ? i : 0)]);
       }
       if constexpr (WM == 2) {
         const double y0 = cone_row0<UC>(ex, G, y);
@@ -666,7 +716,8 @@ BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s
   gdouble* vn = C.at(C.L->vnt);
   struct DL { double d, l; };
   double bad = strided_partial<8, 1>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
-    return (s[i] > 0.0 && z[i] > 0.0) ? 0.0 : 1.0;
+    const double si = s[i], zi = z[i];   // both loaded: no short-circuit branch around z's load
+    return ((si > 0.0) & (zi > 0.0)) ? 0.0 : 1.0;
   });
   gdouble* dli = C.at(C.L->dli);
   struct DLI { double d, di, l; };
@@ -688,13 +739,15 @@ BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s
     const double e = sqrt(sn / zn);
     // v'z without storing v first: v_i = (wbar_i + [i==0]) / nrm
     const double vz = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
-      const double jz = i == 0 ? z[off] : -z[off + i];
+      const double zi = z[off + i];
+      const double jz = i == 0 ? zi : -zi;
       const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
       return (w + (i == 0 ? 1.0 : 0.0)) / nrm * z[off + i];
     }), G.cg);
     struct WV { double w, v, l; };
     strided_batch<4>(G.gl, G.cg, q, [&](int i) {
-      const double jz = i == 0 ? z[off] : -z[off + i];
+      const double zi = z[off + i];
+      const double jz = i == 0 ? zi : -zi;
       const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
       const double v = (w + (i == 0 ? 1.0 : 0.0)) / nrm;
       return WV{w, v, e * (2.0 * v * vz - jz)};
@@ -758,8 +811,10 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
         const int i = G.gl + uu * G.cg;
-        av[uu] = i < q ? ((jconj && i > 0) ? -a[off + i] : a[off + i]) : 0.0;
-        iv[uu] = i < q ? in[off + i] : 0.0;
+        const int ic = off + (i < q ? i : 0);
+        const double m = i < q ? 1.0 : 0.0;
+        av[uu] = (jconj && i > 0 ? -m : m) * a[ic];
+        iv[uu] = m * in[ic];
         part += av[uu] * iv[uu];
       }
       const double dot = ex.gsum(part, G.cg);
@@ -767,7 +822,7 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
         const int i = G.gl + uu * G.cg;
-        adv[uu] = i < q ? ad[off + i] : 0.0;
+        adv[uu] = (i < q ? 1.0 : 0.0) * ad[off + (i < q ? i : 0)];
       }
 #pragma unroll
       for (int uu = 0; uu < UC; ++uu) {
@@ -798,8 +853,10 @@ BMPC_HD void jprod(const X ex, const Ctx& C, const gdouble* u, const gdouble* v,
     BMPC_CONE_K(P, G, k, off, q);
     const double dot = cone_dot(ex, G, u, v, off, q);
     const double u0 = q > 0 ? u[off] : 0.0, v0 = q > 0 ? v[off] : 0.0;
-    strided_batch<4>(G.gl, G.cg, q, [&](int i) { return i == 0 ? dot : u0 * v[off + i] + v0 * u[off + i]; },
-                     [&](int i, double r) { out[off + i] = r; });
+    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+      const double m0 = i == 0 ? 1.0 : 0.0;   // blend, not a select around the loads
+      return m0 * dot + (1.0 - m0) * (u0 * v[off + i] + v0 * u[off + i]);
+    }, [&](int i, double r) { out[off + i] = r; });
   }
   ex.sync();
 }
@@ -816,8 +873,10 @@ BMPC_HD void jdiv(const X ex, const Ctx& C, const gdouble* lam, const gdouble* v
                               G.cg);
     const double l0 = q > 0 ? lam[off] : 1.0;
     const double x0 = q > 0 ? (l0 * v[off] - lv) / rho : 0.0;
-    strided_batch<4>(G.gl, G.cg, q, [&](int i) { return i == 0 ? x0 : (v[off + i] - x0 * lam[off + i]) / l0; },
-                     [&](int i, double r) { out[off + i] = r; });
+    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+      const double m0 = i == 0 ? 1.0 : 0.0;
+      return m0 * x0 + (1.0 - m0) * ((v[off + i] - x0 * lam[off + i]) / l0);
+    }, [&](int i, double r) { out[off + i] = r; });
   }
   ex.sync();
 }
@@ -827,9 +886,8 @@ template <class X>
 BMPC_FN_MAX_STEP double max_step(const X ex, const Ctx Cin, const gdouble* lam, const gdouble* d) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
-  double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
-    return d[i] < 0.0 ? -lam[i] / d[i] : 1e300;
-  });
+  // -lam / min(d, -0): the ratio where d < 0, +inf elsewhere (no branch around the division)
+  double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) { return -lam[i] / fmin(d[i], -0.0); });
   double bad = 0.0;
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
@@ -861,7 +919,7 @@ BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam,
   double a1 = 1e300, a2 = 1e300;
   strided_batch<8>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
     const double l = lam[i], u = d1[i], v = d2[i];
-    return A2{u < 0.0 ? -l / u : 1e300, v < 0.0 ? -l / v : 1e300};
+    return A2{-l / fmin(u, -0.0), -l / fmin(v, -0.0)};   // +inf where the direction is >= 0
   }, [&](int, A2 r) { a1 = fmin(a1, r.a); a2 = fmin(a2, r.b); });
   double bad = 0.0;
   BMPC_CONE_ROUNDS(ex, P, G) {
@@ -1096,16 +1154,18 @@ BMPC_FN_FUSED void combined_rhs(const X ex, const Ctx Cin, const gdouble* lam, g
   const gdouble* eta = C.at(C.L->eta);
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
-    double l[UC], bw[UC], r[UC];
+    double l[UC], bw[UC], r[UC], rzv[UC];
     double pll = 0.0, pdr = 0.0;
 #pragma unroll
-    for (int uu = 0; uu < UC; ++uu) {
+    for (int uu = 0; uu < UC; ++uu) {   // loads unconditional, masked by arithmetic
       const int i = G.gl + uu * G.cg;
       const int ic = off + (i < q ? i : 0);
+      const double m = i < q ? 1.0 : 0.0;
       const double lv = lam[ic], dv = ds[ic], bv = rb[ic];
-      l[uu] = i < q ? lv : 0.0;
-      bw[uu] = i < q ? bv : 0.0;
-      r[uu] = i < q ? dv : 0.0;
+      rzv[uu] = rz[ic];
+      l[uu] = m * lv;
+      bw[uu] = m * bv;
+      r[uu] = m * dv;
       pll += l[uu] * l[uu];
       pdr += r[uu] * bw[uu];
     }
@@ -1151,7 +1211,7 @@ BMPC_FN_FUSED void combined_rhs(const X ex, const Ctx Cin, const gdouble* lam, g
       const int i = G.gl + uu * G.cg;
       if (i < q) {
         ds[off + i] = r[uu];
-        rb[off + i] = l[uu] + eta1 * rz[off + i];
+        rb[off + i] = l[uu] + eta1 * rzv[uu];
       }
     }
   }
@@ -1949,14 +2009,17 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
     row(t, i, isx);
     const gdouble* col = isx ? colk : colnu;
     const size_t cs = isx ? (size_t)P.nv : (size_t)P.neq;
-    double v = isx ? dx[i] : dy[i];
+    const gdouble* src = isx ? dx : dy;   // one load through a selected pointer, not a select of two loads
+    double v = src[i];
     for (int k0 = 0; k0 < nc; k0 += 4) {
-      double c4[4];
+      double c4[4], b4[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) c4[a] = col[(size_t)(k0 + a < nc ? k0 + a : nc - 1) * cs + i];
+      for (int a = 0; a < 4; ++a) {
+        c4[a] = col[(size_t)(k0 + a < nc ? k0 + a : nc - 1) * cs + i];
+        b4[a] = k0 + a < nc ? bc[k0 + a] : 0.0;   // (LDS / uniform: a select here costs no round trip)
+      }
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (k0 + a < nc) v -= bc[k0 + a] * c4[a];
+      for (int a = 0; a < 4; ++a) v -= b4[a] * c4[a];
     }
     return v;
   }, [&](int t, double v) {

@@ -2,6 +2,8 @@
 #include <stdlib.h>
 #include "bmpc_plan.h"
 
+#include <algorithm>
+
 #include <math.h>
 #include <string.h>
 
@@ -308,9 +310,12 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   // finds the system in the slab (Layout::coup) -- deep trees, whose 50 x 50 system would
   // otherwise leave 7 egos per CU.
   const int ncoup = P.nsm * P.nsm + 2 * P.nsm;
+  // the first area holds W1 and Wu (filled at kernel start; the IPM's cone passes index their
+  // rows per lane), at least the 64 doubles of the former reduction area
   P.lds_red = 0;
-  P.lds_scr = 64;
-  P.nscr = desc.controller == BMPC_CTRL_CVAR && 64 + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
+  P.lds_w = 0;
+  P.lds_scr = std::max(64, (n * n + d * d + 7) & ~7);
+  P.nscr = desc.controller == BMPC_CTRL_CVAR && P.lds_scr + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
   P.lds_M = P.lds_scr + P.nscr;
   P.lds_piv = P.lds_M + P.nsm * P.nsm;
   P.lds_rhs = P.lds_piv + P.nsm;

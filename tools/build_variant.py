@@ -12,8 +12,6 @@ from bmpc import _lib  # noqa: E402
 
 tag, flags = sys.argv[1], sys.argv[2:]
 out = os.path.join(os.path.dirname(_lib.SO_PATH), f"libbmpc_{tag}.so")
-cmd = [_lib.HIPCC, f"--offload-arch={_lib.ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-       "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed", *flags,
-       "-I" + _lib.INCLUDE, "-I" + _lib.CSRC, *_lib.sources(), "-o", out]
-subprocess.check_call(cmd)
-print(out)
+_lib.EXTRA_FLAGS[:] = flags
+_lib.SO_PATH = out
+print(_lib.build(force=True))
