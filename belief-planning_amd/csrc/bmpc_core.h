@@ -129,7 +129,9 @@ struct Plan {
   int nsm;    // dense coupling system size
   // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
   int lds_M, lds_piv, lds_rhs, lds_red, nlds;
-  int lds_w;  // W1 (n x n) then Wu (d x d): read with lane-varying rows (apply_G's cone rows)
+  // plan-constant matrices in LDS, read with lane-varying rows (a lane-varying index into the
+  // constant buffer is a vector memory round trip): W1 (n x n), Wu (d x d), Fx (nFx x n), Fu (nFu x d)
+  int lds_w, lds_wu, lds_fx, lds_fu, nconst;
   int nlds_lean;            // LDS doubles when the coupling system lives in the slab (Layout::coup)
   int lds_scr, nscr;       // tree-solve LDS scratch (slack terms of the pre-pass; 0 = none)
   int cgrp;   // lanes per cone group (power of two, cgrp * ceil(ncones / ngrp) covers all cones)
@@ -147,7 +149,11 @@ struct Plan {
 template <class X>
 BMPC_HD double fxv(const BMPC_AS_CONST Plan& P, const X& ex, int r, int j) {
   if constexpr (X::kTransform) return ex.eco[ECO_FX + r * P.n + j];
-  else return P.desc.Fx[r * P.n + j];
+  else return ex.lds[P.lds_fx + r * P.n + j];
+}
+template <class X>
+BMPC_HD double fuv(const BMPC_AS_CONST Plan& P, const X& ex, int r, int j) {
+  return ex.lds[P.lds_fu + r * P.d + j];
 }
 template <class X>
 BMPC_HD double w1v(const BMPC_AS_CONST Plan& P, const X& ex, int r, int j) {
@@ -163,6 +169,14 @@ template <class X>
 BMPC_HD double bxv(const BMPC_AS_CONST Plan& P, const X& ex, int r) {
   if constexpr (X::kTransform) return ex.eco[ECO_BX + r];
   else return P.desc.bx[r];
+}
+
+// entry i of the plan-constant LDS area (Plan::lds_w .. + nconst): W1 | Wu | Fx | Fu
+BMPC_HD double plan_const(const Plan& P, int i) {
+  if (i < P.lds_wu) return P.W1[i - P.lds_w];
+  if (i < P.lds_fx) return P.Wu[i - P.lds_wu];
+  if (i < P.lds_fu) return P.desc.Fx[i - P.lds_fx];
+  return P.desc.Fu[i - P.lds_fu];
 }
 
 // view of the topology tables through ex.tab: the wave's LDS copy of the blob, or the blob in
@@ -186,9 +200,9 @@ struct Layout {
   size_t xbar, zbar, ubar, Ad, Bd, Cd, dh, h0, w, p, dp, boost, xref;
   // IPM vectors
   size_t x, y, z, s, lam, x1, y1, z1, x2, y2, z2, dz, ds, rx, ry, rz, hvec, bvec;
-  size_t ta, ya, ra, rb, rc, bestx;
+  size_t ta, ta2, ya, ra, rb, rc, bestx;
   // KKT-solve scratch
-  size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_cx, k_cy, k_cz, k_nv1, zeros;
+  size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_t3b, k_cx, k_cy, k_cz, k_nv1, zeros;
   // scaling
   size_t dl, dli, eta, wbar, vnt;   // NT scaling: LP d and 1/d, cone eta, wbar, v
   // KKT

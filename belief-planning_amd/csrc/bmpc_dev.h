@@ -113,9 +113,8 @@ template <bool TR, bool TL>
 __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* lds_dyn) {
   const int32_t* gtab = (const int32_t*)P.t.br_depth;   // blob base (the first table)
   double* eco = lds_dyn + (solver_lds_bytes(P, false, TL) / sizeof(double));
-  // W1 | Wu for the cone passes' per-lane row lookups
-  const int nw = P.n * P.n, nwu = P.d * P.d;
-  for (int i = threadIdx.x; i < nw + nwu; i += 64) lds_dyn[P.lds_w + i] = i < nw ? P.W1[i] : P.Wu[i - nw];
+  // W1 | Wu | Fx | Fu for the IPM passes' per-lane row lookups
+  for (int i = threadIdx.x; i < P.nconst; i += 64) lds_dyn[P.lds_w + i] = plan_const(P, i);
   if constexpr (TL) {
     int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
     for (int i = threadIdx.x; i < P.ntab; i += 64) tabl[i] = gtab[i];

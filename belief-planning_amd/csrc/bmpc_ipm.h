@@ -289,11 +289,12 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     const double S = zv[P.oS + it];
     const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
     const int cr = c > 0 ? c - 1 : 0;
+    const double m0 = c == 0 ? 1.0 : 0.0;
     double v = -S;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const double fd = dh[k * NX + j], fx = fxv(P, ex, cr, j);
-      v += (on * (c == 0 ? -fd : fx)) * zv[P.oX + k * NX + j];
+      v += (on * (m0 * (-fd) + (1.0 - m0) * fx)) * zv[P.oX + k * NX + j];   // -fd for c == 0, fx otherwise (exact)
     }
     return Two{lp(P.rFx + it, v), lp(P.rPos + it, -S)};
   }, [&](int it, Two r) { out[P.rFx + it] = r.a; out[P.rPos + it] = r.b; });
@@ -302,7 +303,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     const int u = it / P.nFu, r = it % P.nFu;
     double v = 0.0;
 #pragma unroll
-    for (int j = 0; j < NU; ++j) v += P.desc.Fu[r * NU + j] * zv[P.oU + u * NU + j];
+    for (int j = 0; j < NU; ++j) v += fuv(P, ex, r, j) * zv[P.oU + u * NU + j];
     return lp(P.rFu + it, v);
   }, [&](int it, double v) { out[P.rFu + it] = v; });
   // risk rows: -rho, -mu+, -mu-
@@ -373,7 +374,7 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
     // the weight rows come from LDS (a lane-varying row index into registers would become an
     // indexed private array, i.e. scratch memory): W1 S of this ego or the plan's W1, and Wu
     const ldouble* W1l = X::kTransform ? ex.eco + ECO_W1 : ex.lds + P.lds_w;
-    const ldouble* Wul = ex.lds + P.lds_w + NX * NX;
+    const ldouble* Wul = ex.lds + P.lds_wu;
     auto mid_base = [&](int it) {
       const bool isx = it < nxn;
       const int iu = isx ? 0 : it - nxn;
@@ -1232,13 +1233,14 @@ BMPC_HD int branch_start(CPlan& P, int dep) {
 
 // one Riccati step at a node with input: P = hx + A'Pb A - Qux' Quu^-1 Qux,
 // Quu = hu + B'Pb B (its inverse stored), K = -Quu^-1 Qux (stored).  Pout receives P.
+// The node's data arrive in registers (hx, hu, A, B loaded together by the caller: one memory
+// round trip per node instead of one per operand).
 template <int NX, int NU>
-BMPC_HD bool riccati_step(const gdouble* hx, const gdouble* hu, const gdouble* Ap, const gdouble* Bp,
-                          const double (&Pb)[NX][NX], double (&Pk)[NX][NX], gdouble* Luu_out, gdouble* K_out) {
-  double A[NX][NX], B[NX][NU], M[NX][NX];
-  mat_load(Pk, hx);
-  mat_load(A, Ap);
-  mat_load(B, Bp);
+BMPC_HD bool riccati_step(const double (&Hx)[NX][NX], const double (&Hu)[NU][NU], const double (&A)[NX][NX],
+                          const double (&B)[NX][NU], const double (&Pb)[NX][NX], double (&Pk)[NX][NX],
+                          gdouble* Luu_out, gdouble* K_out) {
+  double M[NX][NX];
+  mat_copy(Hx, Pk);
 #pragma unroll
   for (int i = 0; i < NX; ++i)
 #pragma unroll
@@ -1267,7 +1269,7 @@ BMPC_HD bool riccati_step(const gdouble* hx, const gdouble* hu, const gdouble* A
       for (int r = 0; r < NX; ++r) v += B[r][i] * M[r][j];
       Qux[i][j] = v;
     }
-  mat_load(Quu, hu);
+  mat_copy(Hu, Quu);
 #pragma unroll
   for (int i = 0; i < NU; ++i)
 #pragma unroll
@@ -1459,22 +1461,37 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
       }
       for (int j = len - 1; j >= 0; --j) {
         const int k = ndx + j, u = ndu + j;
+        // every operand of the node first (they do not depend on the recursion)
+        double Hx[NX][NX], Hu[NU][NU], A[NX][NX], B[NX][NU];
+        mat_load(Hx, ws + L.hx + k * NX * NX);
+        mat_load(Hu, ws + L.hu + u * NU * NU);
+        mat_load(A, Ad + u * NX * NX);
+        mat_load(B, Bd + u * NX * NU);
         double Pb[NX][NX];
         if (j < len - 1 || leaf) {
           mat_copy(Pn, Pb);
         } else {
+          // the children's first-node P (written by the previous depth phase), loaded together
           mat_zero(Pb);
           const int c0 = t.br_child0[b];
-          for (int i = 0; i < P.m; ++i) {
-            const gdouble* Pc = ws + L.P + t.br_ndx[c0 + i] * NX * NX;
+          for (int i0 = 0; i0 < P.m; i0 += 2) {
+            double Pc[2][NX][NX];
 #pragma unroll
-            for (int r = 0; r < NX; ++r)
+            for (int h = 0; h < 2; ++h) {
+              const int i = i0 + h < P.m ? i0 + h : i0;
+              mat_load(Pc[h], ws + L.P + t.br_ndx[c0 + i] * NX * NX);
+            }
 #pragma unroll
-              for (int c = 0; c < NX; ++c) Pb[r][c] += Pc[r * NX + c];
+            for (int h = 0; h < 2; ++h) {
+              const double w = i0 + h < P.m ? 1.0 : 0.0;
+#pragma unroll
+              for (int r = 0; r < NX; ++r)
+#pragma unroll
+                for (int c = 0; c < NX; ++c) Pb[r][c] += w * Pc[h][r][c];
+            }
           }
         }
-        if (!riccati_step<NX, NU>(ws + L.hx + k * NX * NX, ws + L.hu + u * NU * NU, Ad + u * NX * NX,
-                                  Bd + u * NX * NU, Pb, Pn, ws + L.Luu + u * NU * NU, ws + L.Kg + u * NU * NX))
+        if (!riccati_step<NX, NU>(Hx, Hu, A, B, Pb, Pn, ws + L.Luu + u * NU * NU, ws + L.Kg + u * NU * NX))
           bad = 1.0;
         mat_store(Pn, ws + L.P + k * NX * NX);
       }
@@ -1599,7 +1616,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         double v = -rr[P.oX + it];
         for (int c = 0; c < Nc; ++c) {
           const double a = sdv[(k * Nc + c) * 2 + 1] * rr[P.oS + k * Nc + c] / sdv[(k * Nc + c) * 2];
-          v -= on * (c == 0 ? -dh[it] : fxv(P, ex, c - 1, j)) * a;
+          const double dhv = dh[it], fx = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
+          v -= on * (m0 * (-dhv) + (1.0 - m0) * fx) * a;
         }
         return v;
       }, [&](int it, double v) { q0[it] = v; });
@@ -1810,7 +1828,10 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
       double fx = 0.0;
 #pragma unroll
-      for (int j = 0; j < NX; ++j) fx += (c == 0 ? -dh[k * NX + j] : fxv(P, ex, c - 1, j)) * o[P.oX + k * NX + j];
+      for (int j = 0; j < NX; ++j) {   // -dh for c == 0, Fx[c-1] otherwise (blend: no branch around the dh load)
+        const double dhv = dh[k * NX + j], fxj = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
+        fx += (m0 * (-dhv) + (1.0 - m0) * fxj) * o[P.oX + k * NX + j];
+      }
       return (rr[P.oS + it] + sdv[it * 2 + 1] * on * fx) / sdv[it * 2];
     }, [&](int it, double v) { o[P.oS + it] = v; });
   }
@@ -1888,16 +1909,21 @@ BMPC_HD auto coup_mem(const X& ex, gdouble* ws, CLayout& L, CPlan& P, int off) {
 // global variable index -> position in the primal vector
 BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
 
-// Woodbury columns, coupling matrix and its LU; returns false on breakdown
+// Woodbury columns, coupling matrix and its LU; returns false on breakdown.  `extra` (0 or 2)
+// more right-hand sides ride in the same tree solve: the z-space slots after the cone vectors
+// (gk + nc nv: the c-direction and affine solves' G'W^-2 r3 + r1), the eq-space slots after the
+// nc zero vectors (bvec, ry), solutions to the slots after the Woodbury columns (x1 / x2,
+// y1 / y2) -- the Riccati data are read once for all of them (Layout, bmpc_plan.cpp).
 template <class X, int NX, int NU>
-BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
+BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_COUPLING);
   gdouble* ws = C.ws;
   const int nc = P.ncones;
-  tree_solve<X, NX, NU>(ex, C, nc, ws + L.gk, P.nv, ws + L.zeros, 0, ws + L.colk, P.nv, ws + L.colnu, P.neq);
+  tree_solve<X, NX, NU>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv, ws + L.colnu,
+                        P.neq);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
   auto* M = coup_mem(ex, ws, L, P, P.lds_M);
   const gdouble* eta = ws + L.eta;
@@ -1960,6 +1986,10 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin) {
   return small_lu(ex, M, coup_mem(ex, ws, L, P, P.lds_piv), ns);
 }
 
+template <class X, int NX, int NU, bool R3ZERO>
+BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble* r2, const gdouble* r3h,
+                      gdouble* dx, gdouble* dy, gdouble* dzh, bool fin);
+
 // One pass of the W-scaled KKT system (oracle/ecos_ipm.py KKT)
 //   [0 A' G'W^-1; A 0 0; W^-1 G 0 -I] [dx; dy; dzh] = [r1; r2; r3h],   dzh = W dz,
 // by the reduced Hessian G'W^-2G (tree Riccati + Woodbury coupling).
@@ -1980,6 +2010,19 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
     apply_GT<X, NX, NU>(ex, C, tr, tz, r1);       // G' W^-1 r3h + r1
   }
   tree_solve<X, NX, NU>(ex, C, 1, tz, 0, r2, 0, dx, 0, dy, 0);
+  kkt_back<X, NX, NU, R3ZERO>(ex, C, tz, r2, r3h, dx, dy, dzh, fin);
+}
+
+// The back half of a KKT solve: with the tree solution (dx, dy) of K [v; nu] = [tz; r2] in
+// place, the Woodbury correction through the coupling system (globals and rank-1 cone terms),
+// then dzh = W^-1 G dx - r3h, or (fin) dz = W^-1 dzh, in one pass.
+template <class X, int NX, int NU, bool R3ZERO>
+BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble* r2, const gdouble* r3h,
+                      gdouble* dx, gdouble* dy, gdouble* dzh, bool fin) {
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* tr = ws + L.k_r0;
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   auto* b = coup_mem(ex, ws, L, P, P.lds_rhs);
   const gdouble* eta = ws + L.eta;
@@ -2040,6 +2083,10 @@ BMPC_HD void kkt_solve_once(const X ex, const Ctx Cin, const gdouble* r1, const 
   else apply_G<X, NX, NU, 1>(ex, C, dx, dzh, r3h, tr);
 }
 
+template <class X, int NX, int NU>
+BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdouble* r2, const gdouble* r3h,
+                        gdouble* dx, gdouble* dy, gdouble* dz, int nitref);
+
 // Solve [0 A' G'; A 0 0; G 0 -W^2] [dx; dy; dz] = [r1; r2; r3]: W-scaled solve with
 // iterative refinement on the scaled residual (well conditioned, unlike the W^2 form whose
 // residual is dominated by the rounding of W^2 dz near the boundary).
@@ -2051,20 +2098,31 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_KKT);
   gdouble* ws = C.ws;
-  gdouble* e1 = ws + L.k_e1;
-  gdouble* e2 = ws + L.k_e2;
-  gdouble* e3 = ws + L.k_e3;
   gdouble* r3h = ws + L.k_t3;
-  gdouble* cx = ws + L.k_cx;
-  gdouble* cy = ws + L.k_cy;
-  gdouble* cz = ws + L.k_cz;
-  gdouble* tv = ws + L.k_nv1;
   apply_Winv2(ex, C, r3, r3h, ws + L.k_r0);      // r3h = W^-1 r3 and kkt_solve_once's W^-1 r3h
   BMPC_COUNT(ws, L, PROF_NSOLVE);
   // without refinement the solve's tail applies the final W^-1 itself
   const bool fin = ex.uniform(nitref == 0);
   kkt_solve_once<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz, true, fin);   // dz holds dzh until the end
   if (fin) return;
+  kkt_refine<X, NX, NU>(ex, C, r1, r2, r3h, dx, dy, dz, nitref);
+}
+
+// Iterative refinement of a W-scaled solve on its scaled residual (nitref > 0 rounds at most),
+// then dz = W^-1 dzh in place (dz holds dzh on entry).
+template <class X, int NX, int NU>
+BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdouble* r2, const gdouble* r3h,
+                        gdouble* dx, gdouble* dy, gdouble* dz, int nitref) {
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* e1 = ws + L.k_e1;
+  gdouble* e2 = ws + L.k_e2;
+  gdouble* e3 = ws + L.k_e3;
+  gdouble* cx = ws + L.k_cx;
+  gdouble* cy = ws + L.k_cy;
+  gdouble* cz = ws + L.k_cz;
+  gdouble* tv = ws + L.k_nv1;
   const double sc = nitref == 0 ? 0.0 : ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
                                      strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
                                 strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
@@ -2098,6 +2156,50 @@ BMPC_FN void kkt_solve(const X ex, const Ctx Cin, const gdouble* r1, const gdoub
   }
   // dz = W^-1 dzh (in place)
   apply_W(ex, C, 1, dz, dz);
+}
+
+// The two KKT solves of an IPM iteration that need only the factorisation -- the c direction
+// [x1; y1; z1] = K^-1 [r1c; bvec; hvec] and the affine direction [x2; y2; z2] = K^-1 [r1a; ry; rb]
+// -- together with the Woodbury columns, in ONE tree solve of nc + 2 right-hand sides
+// (kkt_coupling).  Per right-hand side the arithmetic is that of kkt_solve.  Returns false
+// when the coupling factorisation breaks down.
+template <class X, int NX, int NU>
+BMPC_FN bool kkt_solve_pair(const X ex, const Ctx Cin, const gdouble* r1c, const gdouble* r1a, const gdouble* r3a,
+                            int nitref) {
+  const Ctx C = Cin.uniform();
+  r1c = uniform_ptr(r1c), r1a = uniform_ptr(r1a), r3a = uniform_ptr(r3a);
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_KKT);
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, nc = P.ncones;
+  gdouble* tzc = ws + L.gk + nc * nv;
+  gdouble* tza = tzc + nv;
+  gdouble* r3hc = ws + L.k_t3;
+  gdouble* r3ha = ws + L.k_t3b;
+  gdouble* tr = ws + L.k_r0;
+  const gdouble* bv = ws + L.bvec;
+  const gdouble* ry = ws + L.ry;
+  apply_Winv2(ex, C, ws + L.hvec, r3hc, tr);
+  apply_GT<X, NX, NU>(ex, C, tr, tzc, r1c);
+  apply_Winv2(ex, C, r3a, r3ha, tr);
+  apply_GT<X, NX, NU>(ex, C, tr, tza, r1a);
+  BMPC_COUNT(ws, L, PROF_NSOLVE);
+  BMPC_COUNT(ws, L, PROF_NSOLVE);
+  if (!ex.uniform(kkt_coupling<X, NX, NU>(ex, C, 2))) return false;
+  const bool fin = ex.uniform(nitref == 0);
+  gdouble* x1 = ws + L.x1;
+  gdouble* y1 = ws + L.y1;
+  gdouble* z1 = ws + L.z1;
+  gdouble* x2 = ws + L.x2;
+  gdouble* y2 = ws + L.y2;
+  gdouble* z2 = ws + L.z2;
+  kkt_back<X, NX, NU, false>(ex, C, tzc, bv, r3hc, x1, y1, z1, fin);
+  kkt_back<X, NX, NU, false>(ex, C, tza, ry, r3ha, x2, y2, z2, fin);
+  if (fin) return true;
+  kkt_refine<X, NX, NU>(ex, C, r1c, bv, r3hc, x1, y1, z1, nitref);
+  kkt_refine<X, NX, NU>(ex, C, r1a, ry, r3ha, x2, y2, z2, nitref);
+  return true;
 }
 
 // ECOS bring2cone: s = r + (1 + alpha) e
@@ -2175,6 +2277,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   gdouble* hv = ws + L.hvec;
   gdouble* bv = ws + L.bvec;
   gdouble* tA = ws + L.ta;
+  gdouble* tA2 = ws + L.ta2;
   gdouble* ya = ws + L.ya;
   gdouble* ra = ws + L.ra;
   gdouble* rb = ws + L.rb;
@@ -2188,7 +2291,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   build_hb<X, NX, NU>(ex, C, hv, bv);
   // ---- initial point with W = I ----------------------------------------------------------
   identity_scaling(ex, C);
-  if (!kkt_factor<X, NX, NU>(ex, C, true) || !kkt_coupling<X, NX, NU>(ex, C)) {
+  if (!kkt_factor<X, NX, NU>(ex, C, true) || !kkt_coupling<X, NX, NU>(ex, C, 0)) {
     res.exit_flag = EXIT_NUMERICS;
     return res;
   }
@@ -2334,22 +2437,21 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     // branches scalar, so no phase is ever called under a partial exec mask
     bool ok = ex.uniform(compute_scaling(ex, C, s, z));
     if (ok) ok = ex.uniform(kkt_factor<X, NX, NU>(ex, C, false));
-    if (ok) ok = ex.uniform(kkt_coupling<X, NX, NU>(ex, C));
     double alpha = 0.0, dtau = 0.0, dkap = 0.0;
     // refinement only once the iterate nears the tolerances: an unrefined direction is
     // accurate to ~1e-12 relative, far below what the early steps need
     const int nref = score < BMPC_REFSCORE2 ? BMPC_NITREF2 : score < BMPC_REFSCORE ? BMPC_NITREF : 0;
     if (ok) {
-      // c vector
+      // right-hand sides of the c direction (-c, bvec, hvec) and the affine direction
+      // (-rx, ry, rb = rz - W xi = rz + W lam for xi = -lam), solved together with the
+      // Woodbury columns (kkt_solve_pair)
       lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
-      ex.sync();
-      kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x1, y1, z1, nref);
-      const double den = kap / tau - (x1[P.oJ] + dot2(ex, bv, y1, neq, hv, z1, nr));
-      // affine: xi = -lam, rb = rz - W xi = rz + W lam
+      lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA2[i] = v; });
       apply_W(ex, C, 0, lam, rb, 1.0, rz, 1.0);
-      lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA[i] = v; });
-      ex.sync();
-      kkt_solve<X, NX, NU>(ex, C, tA, ry, rb, x2, y2, z2, nref);
+      ok = ex.uniform(kkt_solve_pair<X, NX, NU>(ex, C, tA, tA2, rb, nref));
+    }
+    if (ok) {
+      const double den = kap / tau - (x1[P.oJ] + dot2(ex, bv, y1, neq, hv, z1, nr));
       const double dk_aff = -kap * tau;
       const double dtau_a = (rt + dk_aff / tau + x2[P.oJ] + dot2(ex, bv, y2, neq, hv, z2, nr)) / den;
       // dz_aff = z2 + dtau_a z1, rb = W dz_aff, ds = dsW_aff = xi - W dz_aff (one pass)

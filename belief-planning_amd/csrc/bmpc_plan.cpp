@@ -314,7 +314,11 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   // rows per lane), at least the 64 doubles of the former reduction area
   P.lds_red = 0;
   P.lds_w = 0;
-  P.lds_scr = std::max(64, (n * n + d * d + 7) & ~7);
+  P.lds_wu = P.lds_w + n * n;
+  P.lds_fx = P.lds_wu + d * d;
+  P.lds_fu = P.lds_fx + P.nFx * n;
+  P.nconst = P.lds_fu + P.nFu * d;
+  P.lds_scr = std::max(64, (P.nconst + 7) & ~7);
   P.nscr = desc.controller == BMPC_CTRL_CVAR && P.lds_scr + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
   P.lds_M = P.lds_scr + P.nscr;
   P.lds_piv = P.lds_M + P.nsm * P.nsm;
@@ -386,20 +390,15 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.z = take(nr);
   L.s = take(nr);
   L.lam = take(nr);
-  L.x1 = take(nv);
-  L.y1 = take(neq);
   L.z1 = take(nr);
-  L.x2 = take(nv);
-  L.y2 = take(neq);
   L.z2 = take(nr);
   L.dz = take(nr);
   L.ds = take(nr);
   L.rx = take(nv);
-  L.ry = take(neq);
   L.rz = take(nr);
   L.hvec = take(nr);
-  L.bvec = take(neq);
   L.ta = take(nv);
+  L.ta2 = take(nv);
   L.ya = take(neq);
   L.ra = take(nr);
   L.rb = take(nr);
@@ -411,11 +410,11 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.k_e2 = take(neq);
   L.k_e3 = take(nr);
   L.k_t3 = take(nr);
+  L.k_t3b = take(nr);
   L.k_cx = take(nv);
   L.k_cy = take(neq);
   L.k_cz = take(nr);
   L.k_nv1 = take(nv);
-  L.zeros = take(neq);   // all-zero eq-space vector (tree solves without an e term)
   L.dl = take(P.nlp);
   L.dli = take(P.nlp);
   L.eta = take(nc);
@@ -427,12 +426,39 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.P = take((size_t)T * n * n);
   L.Kg = take((size_t)U * d * n);
   L.Luu = take((size_t)U * d * d);
-  L.kff = take((size_t)(nc > 0 ? nc : 1) * U * d);   // (PROX: one rhs)
-  L.lvec = take((size_t)(nc > 0 ? nc : 1) * T * n);
-  L.qx0 = take((size_t)(nc > 0 ? nc : 1) * T * n);   // slack-eliminated x rhs of the tree sweeps
-  L.gk = take((size_t)nc * nv);
-  L.colk = take((size_t)nc * nv);
-  L.colnu = take((size_t)nc * neq);
+  // tree-solve right-hand sides (CVaR: the nc Woodbury columns plus the c-direction and affine
+  // solves that ride in the same tree solve, kkt_coupling / kkt_solve_pair)
+  const size_t nrhs = nc > 0 ? (size_t)nc + 2 : 1;
+  L.kff = take(nrhs * U * d);
+  L.lvec = take(nrhs * T * n);
+  L.qx0 = take(nrhs * T * n);   // slack-eliminated x rhs of the tree sweeps
+  if (nc > 0) {
+    // contiguous rhs / solution blocks of the merged tree solve, stride nv (z-space) / neq
+    // (eq-space): g_1..g_nc | tz_c | tz_a,  col_1..col_nc | x1 | x2,  colnu_1..nc | y1 | y2,
+    // and the eq-space rhs 0 (nc times) | bvec | ry
+    L.gk = take((size_t)(nc + 2) * nv);
+    const size_t colk = take((size_t)(nc + 2) * nv);
+    L.colk = colk;
+    L.x1 = colk + (size_t)nc * nv;
+    L.x2 = L.x1 + nv;
+    const size_t colnu = take((size_t)(nc + 2) * neq);
+    L.colnu = colnu;
+    L.y1 = colnu + (size_t)nc * neq;
+    L.y2 = L.y1 + neq;
+    const size_t zb = take((size_t)(nc + 2) * neq);
+    L.zeros = zb;                        // nc all-zero eq-space vectors (never written)
+    L.bvec = zb + (size_t)nc * neq;
+    L.ry = L.bvec + neq;
+  } else {
+    L.gk = L.colk = L.colnu = take(0);
+    L.x1 = take(nv);
+    L.y1 = take(neq);
+    L.x2 = take(nv);
+    L.y2 = take(neq);
+    L.ry = take(neq);
+    L.bvec = take(neq);
+    L.zeros = take(neq);   // all-zero eq-space vector (tree solves without an e term)
+  }
   L.prof = take(PROF_COUNT);
   L.coup = take((size_t)P.nsm * P.nsm + 2 * (size_t)P.nsm);
   if (desc.controller != BMPC_CTRL_CVAR) {   // QP-only arrays (augmented-state Riccati)

@@ -27,10 +27,17 @@ struct QpCtx {
 template <class T>
 BMPC_HD int qp_pred_u(const T& t, int u) { return t.x_srcu[t.u_x[u]]; }
 
-// coefficient j of inequality row c of state node k: Ncol collision rows (-dh) then the Fx rows
-template <int NX>
-BMPC_HD double qp_row(CPlan& P, const gdouble* dh, int k, int c, int j) {
-  return c < P.Ncol ? -dh[((size_t)k * P.Ncol + c) * NX + j] : P.desc.Fx[(c - P.Ncol) * NX + j];
+// coefficient j of inequality row c of state node k: Ncol collision rows (-dh) then the Fx rows.
+// Branch-free: both operands are read (clamped indices; Fx from the plan-constant LDS area) and
+// blended exactly -- a select would become a branch around the dh load (one memory round trip
+// per coefficient).
+template <int NX, class X>
+BMPC_HD double qp_row(CPlan& P, const X& ex, const gdouble* dh, int k, int c, int j) {
+  const bool col = c < P.Ncol;
+  const double d = dh[((size_t)k * P.Ncol + (col ? c : 0)) * NX + j];
+  const double f = fxv(P, ex, col ? 0 : c - P.Ncol, j);
+  const double m = col ? 1.0 : 0.0;
+  return m * (-d) + (1.0 - m) * f;
 }
 // rows of state node k are live: every node with an input, and robustMPC's terminal node
 // (its Fx rows carry slacks, MPC_branch.py:1470-1472); BranchMPC's leaf terminals are empty
@@ -207,14 +214,15 @@ BMPC_FN void qp_apply_G(const X ex, const QpCtx Cin, const gdouble* zv, gdouble*
   lane_batch(ex, 0, P.T * Nc, [&](int it) {
     const int k = it / Nc, c = it % Nc;
     double v = -zv[P.oS + it];
-    if (qp_rows_on(P, t, k))
-      for (int j = 0; j < NX; ++j) v += qp_row<NX>(P, dh, k, c, j) * zv[P.oX + k * NX + j];
+    const double on = qp_rows_on(P, t, k) ? 1.0 : 0.0;   // multiplier, not a branch around the loads
+#pragma unroll
+    for (int j = 0; j < NX; ++j) v += on * qp_row<NX>(P, ex, dh, k, c, j) * zv[P.oX + k * NX + j];
     return v;
   }, [&](int it, double v) { out[P.rFx + it] = v; });
   lane_batch(ex, 0, P.U * P.nFu, [&](int it) {
     const int u = it / P.nFu, r = it % P.nFu;
     double v = 0.0;
-    for (int j = 0; j < NU; ++j) v += P.desc.Fu[r * NU + j] * zv[P.oU + u * NU + j];
+    for (int j = 0; j < NU; ++j) v += fuv(P, ex, r, j) * zv[P.oU + u * NU + j];
     return v;
   }, [&](int it, double v) { out[P.rFu + it] = v; });
   lane_batch(ex, 0, P.T * Nc, [&](int it) { return -zv[P.oS + it]; }, [&](int it, double v) { out[P.rPos + it] = v; });
@@ -237,7 +245,7 @@ BMPC_FN void qp_apply_GT(const X ex, const QpCtx Cin, const gdouble* r, gdouble*
     for (int c = 0; c < Nc; ++c) {
       const double rv = r[P.rFx + k * Nc + c];
       if (qp_rows_on(P, t, k))
-        for (int j = 0; j < NX; ++j) ax[j] += qp_row<NX>(P, dh, k, c, j) * rv;
+        for (int j = 0; j < NX; ++j) ax[j] += qp_row<NX>(P, ex, dh, k, c, j) * rv;
       out[P.oS + k * Nc + c] = -rv - r[P.rPos + k * Nc + c];
     }
     for (int j = 0; j < NX; ++j) out[P.oX + k * NX + j] = ax[j];
@@ -349,7 +357,7 @@ BMPC_FN bool qp_factor(const X ex, const QpCtx Cin, const gdouble* dinv) {
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double om = df - df * df / sd;
             double f[NX];
-            for (int j = 0; j < NX; ++j) f[j] = qp_row<NX>(P, dh, k, c, j);
+            for (int j = 0; j < NX; ++j) f[j] = qp_row<NX>(P, ex, dh, k, c, j);
             for (int i = 0; i < NX; ++i)
               for (int j = 0; j < NX; ++j) Hx[i][j] += om * f[i] * f[j];
           }
@@ -481,7 +489,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
           for (int c = 0; c < Nc; ++c) {   // slack elimination
             const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
             const double a = df * r[P.oS + k * Nc + c] / sd;
-            for (int j = 0; j < NX; ++j) qx[j] -= qp_row<NX>(P, dh, k, c, j) * a;
+            for (int j = 0; j < NX; ++j) qx[j] -= qp_row<NX>(P, ex, dh, k, c, j) * a;
           }
         double lt[NS];
         if (term) {
@@ -565,7 +573,7 @@ BMPC_FN void qp_tree_solve(const X ex, const QpCtx Cin, const gdouble* r, const 
           const double sd = ws[L.sd + (k * Nc + c) * 2], df = ws[L.sd + (k * Nc + c) * 2 + 1];
           double fx = 0.0;
           if (qp_rows_on(P, t, k))
-            for (int j = 0; j < NX; ++j) fx += qp_row<NX>(P, dh, k, c, j) * s[j];
+            for (int j = 0; j < NX; ++j) fx += qp_row<NX>(P, ex, dh, k, c, j) * s[j];
           out[P.oS + k * Nc + c] = (r[P.oS + k * Nc + c] + df * fx) / sd;
         }
         if (term) break;

@@ -120,7 +120,7 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   const char* lean_env = getenv("BMPC_HOST_LEAN");
   const bool lean = lean_env && atoi(lean_env) != 0;
   std::vector<double> lds(P.nlds), eco(ECO_COUNT);
-  for (int i = 0; i < P.n * P.n + P.d * P.d; ++i) lds[P.lds_w + i] = i < P.n * P.n ? P.W1[i] : P.Wu[i - P.n * P.n];
+  for (int i = 0; i < P.nconst; ++i) lds[P.lds_w + i] = plan_const(P, i);
   ex.lds = exm.lds = exl.lds = lds.data();
   ex.tab = exm.tab = exl.tab = P.t.br_depth;      // the host blob (first table at offset 0)
   exm.eco = eco.data();
