@@ -28,7 +28,8 @@ def sources():
     """Translation units of libbmpc.so: the C ABI + small kernels, one unit per predictive model's
     solver kernels (compiled in parallel), the host-side plan builders."""
     return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_k_highway.hip", "bmpc_k_highway_t.hip",
-                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_plan.cpp",
+                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_kp_highway.hip",
+                                            "bmpc_kp_highway_t.hip", "bmpc_kp_merge.hip", "bmpc_plan.cpp",
                                             "bmpc_qpplan.cpp")]
 
 

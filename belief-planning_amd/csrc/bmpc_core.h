@@ -207,7 +207,9 @@ struct Layout {
   size_t dl, dli, eta, wbar, vnt;   // NT scaling: LP d and 1/d, cone eta, wbar, v
   // KKT
   size_t hx, hu, sd, P, Kg, Luu, kff, lvec, qx0, gk, colk, colnu;
-  size_t coup;    // coupling matrix | pivots | rhs when they are not in LDS (lean-LDS launches)
+  size_t coup;    // coupling matrix | pivots | rhs when they are not in LDS (lean-LDS launches; the
+                  // phase-per-kernel IPM keeps the factored matrix and pivots here between kernels)
+  size_t ist;     // the phase-per-kernel IPM's per-ego state (IS_* slots, bmpc_ipm_ph.h)
   size_t prof;    // PROF_COUNT phase cycle counters (BMPC_PROFILE builds)
   // BranchMPCProx QP: u-rate couplings, linear cost, augmented Riccati P~, [Kx Kv], l~
   size_t qo, qq, Pa, Ka, la;

@@ -210,6 +210,11 @@ struct SolveLaunch {
   bool rich;          // LDS-rich solver launch (choose_lds_rich)
   bool qp;            // OSQP-class controller (k_qp) instead of the CVaR IPM (k_ipm)
   hipStream_t stream;
+  // phase-per-kernel IPM (bmpc_dev_ph.h): per-iteration "egos going on" counters, their pinned
+  // read-back slot, the iteration limit
+  int32_t* d_count = nullptr;
+  int32_t* h_count = nullptr;
+  int maxit = 0;
 };
 
 template <class M>
@@ -250,6 +255,10 @@ hipError_t launch_tree_merge(const SolveLaunch& a);
 hipError_t launch_solver_merge(const SolveLaunch& a);
 hipError_t launch_tree_quadruped(const SolveLaunch& a);
 hipError_t launch_solver_quadruped(const SolveLaunch& a);
+// the phase-per-kernel CVaR IPM (bmpc_kp_*.hip)
+hipError_t launch_ipm_phased_highway(const SolveLaunch& a);
+hipError_t launch_ipm_phased_highway_t(const SolveLaunch& a);
+hipError_t launch_ipm_phased_merge(const SolveLaunch& a);
 
 }  // namespace dev
 }  // namespace bmpc

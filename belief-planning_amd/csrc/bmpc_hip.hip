@@ -16,6 +16,10 @@
 using namespace bmpc;
 using namespace bmpc::dev;
 
+#ifndef BMPC_IPM_PHASED_DEFAULT
+#define BMPC_IPM_PHASED_DEFAULT 0
+#endif
+
 namespace {
 
 // LDS-rich launch (topology tables and coupling system in LDS) only when it costs no
@@ -181,6 +185,8 @@ struct bmpc_plan {
   double t_acc[2] = {0, 0};
   int t_cnt = 0;
   bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
+  int32_t* d_count = nullptr;   // phase-per-kernel IPM: egos going on per iteration [maxit + 1]
+  int32_t* h_count = nullptr;   // ... its pinned read-back slot
 };
 
 extern "C" {
@@ -231,7 +237,9 @@ int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_
       hipMalloc(&pl->d_pol, sizeof(bmpc_policy) * (size_t)batch * P.m) != hipSuccess ||
       hipMalloc(&pl->d_in, sizeof(double) * (size_t)batch * P.n * 3) != hipSuccess ||
       hipMalloc(&pl->d_out, sizeof(double) * (size_t)batch * ((size_t)P.U * P.d + (size_t)P.T * P.n + P.nbranch + 1)) != hipSuccess ||
-      hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess)
+      hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess ||
+      hipMalloc(&pl->d_count, sizeof(int32_t) * (size_t)(P.desc.maxit + 1)) != hipSuccess ||
+      hipHostMalloc(&pl->h_count, sizeof(int32_t)) != hipSuccess)
     return cleanup(fail(-12, "hipMalloc failed (out of device memory?)"));
   if (hipMemcpy(pl->d_tables, pl->hp.blob.data(), pl->hp.blob.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(-5, "hipMemcpy tables failed"));
@@ -269,6 +277,8 @@ int bmpc_plan_destroy(bmpc_plan* pl) {
   hipFree(pl->d_out);
   hipFree(pl->d_iout);
   hipFree(pl->d_scratch);
+  hipFree(pl->d_count);
+  if (pl->h_count) hipHostFree(pl->h_count);
   for (auto& e : pl->ev)
     if (e) hipEventDestroy(e);
   if (pl->stream) hipStreamDestroy(pl->stream);
@@ -365,6 +375,11 @@ static int fold_timing(bmpc_plan* pl) {
   return 0;
 }
 
+static bool use_phased() {
+  const char* e = getenv("BMPC_IPM_PHASED");
+  return e ? atoi(e) != 0 : BMPC_IPM_PHASED_DEFAULT;
+}
+
 static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
                         double* d_upred, double* d_xpred, double* d_bw, double* d_J,
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
@@ -384,13 +399,22 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   }
   if (pl->timing && (pl->t_pending < 0 || pl->t_pending >= bmpc_plan::kTimeSlots))
     return fail(-5, "timing ring out of range (t_pending = " + std::to_string(pl->t_pending) + ")");
-  const SolveLaunch a{pl->d_bundle, pl->d_ws, pl->d_pol, d_x, d_z, d_xref, d_upred, d_xpred, d_bw, d_J, d_status,
-                      d_iters, B, lds_bytes, tl, P.desc.controller != BMPC_CTRL_CVAR, s};
+  SolveLaunch a{pl->d_bundle, pl->d_ws, pl->d_pol, d_x, d_z, d_xref, d_upred, d_xpred, d_bw, d_J, d_status,
+                d_iters, B, lds_bytes, tl, P.desc.controller != BMPC_CTRL_CVAR, s};
+  a.d_count = pl->d_count;
+  a.h_count = pl->h_count;
+  a.maxit = P.desc.maxit;
   hipError_t (*tree)(const SolveLaunch&) = launch_tree_quadruped;
   hipError_t (*solver)(const SolveLaunch&) = launch_solver_quadruped;
-  if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t;
-  else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway;
-  else if (merge) tree = launch_tree_merge, solver = launch_solver_merge;
+  hipError_t (*phased)(const SolveLaunch&) = nullptr;
+  if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t, phased = launch_ipm_phased_highway_t;
+  else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway, phased = launch_ipm_phased_highway;
+  else if (merge) tree = launch_tree_merge, solver = launch_solver_merge, phased = launch_ipm_phased_merge;
+  // the CVaR IPM runs phase per kernel (bmpc_dev_ph.h) when its plan's LDS-rich layout is the
+  // launch's (the factored coupling system is re-read into LDS by each kernel that solves with it);
+  // BMPC_IPM_PHASED=0 selects the monolithic k_ipm
+  if (phased && (P.desc.controller != BMPC_CTRL_CVAR || !tl || !use_phased())) phased = nullptr;
+  if (phased) solver = phased;
   hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));
   HIPCHECK(tree(a));

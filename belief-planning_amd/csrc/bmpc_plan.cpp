@@ -461,6 +461,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   }
   L.prof = take(PROF_COUNT);
   L.coup = take((size_t)P.nsm * P.nsm + 2 * (size_t)P.nsm);
+  L.ist = take(64);
   if (desc.controller != BMPC_CTRL_CVAR) {   // QP-only arrays (augmented-state Riccati)
     const int NS = n + d;
     L.qo = take((size_t)U * d * d);

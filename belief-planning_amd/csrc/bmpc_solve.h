@@ -10,14 +10,14 @@
 
 namespace bmpc {
 
-// phase 2: IPM + unpack (reads the tree written by tree_update; xref copied there)
+// once per solve, before the IPM: the first solve freezes Jcons = xRef Q xRef
+// (MPC_branch.py:1939); transform plans write their state rows Fx S / bx (below)
 template <class X, class M>
-BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, EgoView E) {
-  constexpr int NX = M::NX, NU = M::NU;
-  double* ws = E.ws;
+BMPC_HD void ipm_prelude(const X& ex, const Plan& P, const Layout& L, double* ws) {
+  constexpr int NX = M::NX;
   const bool init = ws[L.misc + MISC_INIT] != 0.0;
   const double* xref = ws + L.xref;
-  if (!init && ex.lane == 0) {   // first solve freezes Jcons = xRef Q xRef (MPC_branch.py:1939)
+  if (!init && ex.lane == 0) {
     double j = 0.0;
     for (int c = 0; c < NX; ++c) {
       double v = 0.0;
@@ -27,11 +27,10 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
     ws[L.misc + MISC_JCONS] = j;
   }
   if constexpr (X::kTransform) {
-    // per-ego constants of this solve.  State rows and their bound: Fx S / bx (Fx without S)
-    // from the current Fx and bx, written by buildIneqConstr on the first solve
-    // (MPC_branch.py:1894-1901) and by updateIneqConstr only while S is on (:2025-2036) --
-    // with S off a later solve keeps the rows it finds (:2016-2024 patch the collision row
-    // alone).  The cone rows use W1 S (W1 without S) on every solve (:1935-1937, :1995-1998).
+    // State rows and their bound: Fx S / bx (Fx without S) from the current Fx and bx, written
+    // by buildIneqConstr on the first solve (MPC_branch.py:1894-1901) and by updateIneqConstr
+    // only while S is on (:2025-2036) -- with S off a later solve keeps the rows it finds
+    // (:2016-2024 patch the collision row alone).
     double* xf = ws + L.xform;
     const bool son = xf[XF_SON] != 0.0, bxset = xf[XF_BXSET] != 0.0, fxset = xf[XF_FXSET] != 0.0;
     const bool rewrite = !init || son || xf[XF_ROWSET] == 0.0;
@@ -56,6 +55,21 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
       ex.sync();
       if (ex.lane == 0) xf[XF_ROWSET] = 1.0;
     }
+  }
+  ex.sync();
+}
+
+// per-ego constants of this solve in the wave's LDS (X::kTransform): the state rows written by
+// ipm_prelude, W1 S (W1 without S) for the cone rows on every solve (:1935-1937, :1995-1998),
+// (W1 S)'(W1 S) and bx.  Every kernel that runs a part of the IPM forms them on entry.
+template <class X, class M>
+BMPC_HD void ipm_eco(const X& ex, const Plan& P, const Layout& L, const double* ws) {
+  constexpr int NX = M::NX;
+  if constexpr (X::kTransform) {
+    const double* xf = ws + L.xform;
+    const bool son = xf[XF_SON] != 0.0;
+    const double* S = xf + XF_S;
+    const int nF = P.nFx;
     for (int i = ex.lane; i < nF * NX + 2 * NX * NX + nF; i += ex.nlanes) {
       double v;
       if (i < nF * NX) {
@@ -89,13 +103,14 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
       }
     }
   }
-  Ctx C;
-  C.P = (CPlan*)&P;
-  C.L = (CLayout*)&L;
-  C.ws = (gdouble*)ws;
   ex.sync();
-  IpmResult r = ipm_solve<X, NX, NU>(ex, C);
-  // ---- unpack -----------------------------------------------------------------------------
+}
+
+// unpackSolution (MPC_branch.py:2096-2106) with the "keep the previous solution when
+// infeasible" rule, OldInput = uPred[0]
+template <class X, class M>
+BMPC_HD void ipm_unpack(const X& ex, const Plan& P, const Layout& L, double* ws, const IpmResult& r) {
+  constexpr int NX = M::NX, NU = M::NU;
   const double* sol = ws + L.sol;
   const bool feasible = r.exit_flag >= 0;
   if (feasible) {
@@ -114,6 +129,21 @@ BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, Ego
     for (int i = 0; i < NU; ++i) ws[L.misc + MISC_OLDU + i] = ws[L.upred + i];
   }
   ex.sync();
+}
+
+// phase 2: IPM + unpack (reads the tree written by tree_update; xref copied there)
+template <class X, class M>
+BMPC_HD IpmResult solve_ego_ipm(const X& ex, const Plan& P, const Layout& L, EgoView E) {
+  constexpr int NX = M::NX, NU = M::NU;
+  double* ws = E.ws;
+  ipm_prelude<X, M>(ex, P, L, ws);
+  ipm_eco<X, M>(ex, P, L, ws);
+  Ctx C;
+  C.P = (CPlan*)&P;
+  C.L = (CLayout*)&L;
+  C.ws = (gdouble*)ws;
+  IpmResult r = ipm_solve<X, NX, NU>(ex, C);
+  ipm_unpack<X, M>(ex, P, L, ws, r);
   return r;
 }
 

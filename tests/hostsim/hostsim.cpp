@@ -13,6 +13,7 @@
 #include "bmpc_plan.h"
 #include "bmpc_hmm.h"
 #include "bmpc_solve.h"
+#include "bmpc_ipm_ph.h"
 #include "bmpc_env.h"
 #include "bmpc_qpplan.h"
 
@@ -50,6 +51,15 @@ struct HostExecT {
   double min(double v) const { return v; }
 };
 using HostExec = HostExecT<false>;
+
+// BMPC_HOST_PHASED=1: CVaR solves through the phase sequence of the GPU's phase-per-kernel IPM
+template <class X, class M>
+IpmResult hs_solve_ego(const X& ex, const Plan& P, const Layout& L, EgoView E, const double* x, const double* z,
+                       const double* xref, bool phased, std::vector<double>& lds) {
+  if (!phased || P.desc.controller != BMPC_CTRL_CVAR) return solve_ego<X, M>(ex, P, L, E, x, z, xref);
+  tree_step<X, M>(ex, P, L, E, x, z, xref);
+  return solve_ego_ipm_phased<X, M>(ex, P, L, E, lds.data(), (int)lds.size());
+}
 
 struct HS {
   HostPlan hp;
@@ -119,6 +129,8 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
   HostExecT<false, false> exl;          // BMPC_HOST_LEAN=1: the lean-LDS launch's slab coupling system
   const char* lean_env = getenv("BMPC_HOST_LEAN");
   const bool lean = lean_env && atoi(lean_env) != 0;
+  const char* ph_env = getenv("BMPC_HOST_PHASED");
+  const bool phased = ph_env && atoi(ph_env) != 0;
   std::vector<double> lds(P.nlds), eco(ECO_COUNT);
   for (int i = 0; i < P.nconst; ++i) lds[P.lds_w + i] = plan_const(P, i);
   ex.lds = exm.lds = exl.lds = lds.data();
@@ -129,15 +141,15 @@ int hs_solve(void* p, const double* x, const double* z, const double* xref, doub
     EgoView E{h->ws.data() + L.stride * e, h->pol.data() + (size_t)e * P.m};
     IpmResult r;
     if (P.desc.model == BMPC_MODEL_HIGHWAY && (P.desc.flags & BMPC_PLAN_TRANSFORM))
-      r = solve_ego<HostExecT<true>, HighwayT>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
-    else if (P.desc.model == BMPC_MODEL_HIGHWAY && lean)
+      r = hs_solve_ego<HostExecT<true>, HighwayT>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n, phased, lds);
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY && lean && !phased)
       r = solve_ego<HostExecT<false, false>, Highway>(exl, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
     else if (P.desc.model == BMPC_MODEL_HIGHWAY)
-      r = solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+      r = hs_solve_ego<HostExec, Highway>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n, phased, lds);
     else if (P.desc.model == BMPC_MODEL_HIGHWAY_MERGE)
-      r = solve_ego<HostExecT<true>, HighwayMerge>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+      r = hs_solve_ego<HostExecT<true>, HighwayMerge>(exm, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n, phased, lds);
     else
-      r = solve_ego<HostExec, Quadruped>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n);
+      r = hs_solve_ego<HostExec, Quadruped>(ex, P, L, E, x + e * P.n, z + e * P.n, xref + e * P.n, phased, lds);
     const double* ws = E.ws;
     if (upred) memcpy(upred + (size_t)e * P.U * P.d, ws + L.upred, sizeof(double) * P.U * P.d);
     if (xpred) memcpy(xpred + (size_t)e * P.T * P.n, ws + L.xpred, sizeof(double) * P.T * P.n);

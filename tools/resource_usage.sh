@@ -2,9 +2,9 @@
 # compiler's per-kernel / per-function resource report (VGPRs, spills, scratch, LDS, occupancy)
 # of the highway model's solver translation unit (k_tree, k_ipm, k_qp and the out-of-line
 # device functions they call).
-# usage: tools/resource_usage.sh [-DFLAG ...]   (MODEL=merge|quadruped|highway_t picks another TU)
+# usage: tools/resource_usage.sh [-DFLAG ...]   (MODEL=merge|quadruped|highway_t picks another TU; TU=bmpc_kp_highway.hip names one)
 cd "$(dirname "$0")/.."
-tu=belief-planning_amd/csrc/bmpc_k_${MODEL:-highway}.hip
+tu=belief-planning_amd/csrc/${TU:-bmpc_k_${MODEL:-highway}.hip}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -c -o /tmp/ru_$$.o \
   -Wno-unused-value -Wno-unused-result -Wno-pass-failed -Rpass-analysis=kernel-resource-usage "$@" \
   -Iinclude -Ibelief-planning_amd/csrc "$tu" > /tmp/ru_$$.log 2>&1
