@@ -93,6 +93,8 @@ struct DevExecT {
 
 using DevExec = DevExecT<false>;
 
+constexpr int kMaxSub = 8;   // sub-batch streams of the phase-per-kernel IPM
+
 struct Bundle {
   Plan P;
   Layout L;
@@ -215,6 +217,10 @@ struct SolveLaunch {
   int32_t* d_count = nullptr;
   int32_t* h_count = nullptr;
   int maxit = 0;
+  int ph_mode = 1;   // 1: one kernel per phase, 2: one kernel calling grouped out-of-line phases
+  int nsub = 1;                   // mode 1: sub-batches, one stream each
+  hipStream_t* sub = nullptr;     // their streams [kMaxSub]
+  hipEvent_t* sub_ev = nullptr;   // [kMaxSub + 1] fork / join events
 };
 
 template <class M>

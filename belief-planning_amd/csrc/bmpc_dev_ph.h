@@ -27,14 +27,15 @@ struct PhArgs {
   double* ws;
   double *upred, *xpred, *bw, *J;
   int32_t *status, *iters;
-  int32_t* count;   // [maxit + 1]: egos that completed iteration it's step
-  int batch;
+  int32_t* count;   // [maxit + 1]: egos of this sub-batch that completed iteration it's step
+  int e0;           // first ego of the sub-batch this launch covers
+  int batch;        // egos in it
 };
 
 template <class M, int PH>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ph(const PhArgs a, int it) {
-  const int e = blockIdx.x;
-  if (e >= a.batch) return;
+  if ((int)blockIdx.x >= a.batch) return;
+  const int e = a.e0 + blockIdx.x;
   const Plan& P = a.B->P;
   const Layout& L = a.B->L;
   double* ws = a.ws + L.stride * (size_t)e;
@@ -94,52 +95,185 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   }
 }
 
+// ---- mode 2: one kernel, a handful of out-of-line phase functions per iteration -------------
+// Each out-of-line device call costs its callee-saved-register round trip through scratch; the
+// monolithic k_ipm makes ~24 per IPM iteration (every operator pass is its own function).  Here
+// an iteration makes at most seven -- RES, FAC+CPL+BKP, AFF+CMB, UPD and the refinement rounds
+// that run -- each with every operator inlined into it.
+template <class X, int NX, int NU, int G>
+__device__ __attribute__((noinline)) bool ph_group(const X ex, const Ctx Cin, int it) {
+  // arguments arrive in VGPRs: the plan / layout / slab pointers back to SGPRs (scalar loads of
+  // every Plan field instead of vector loads)
+  const Ctx C = Cin.uniform();
+  it = __builtin_amdgcn_readfirstlane(it);
+  const gdouble* st = C.ws + C.L->ist;
+  if constexpr (G == 0) {   // initial point
+    ph_init1<X, NX, NU>(ex, C);
+    if (ph_flag(ex, st, IS_OK)) ph_init2<X, NX, NU>(ex, C);
+    if (ph_flag(ex, st, IS_OK)) ph_init3<X, NX, NU>(ex, C);
+  } else if constexpr (G == 1) {
+    ph_res<X, NX, NU>(ex, C, it);
+  } else if constexpr (G == 2) {   // factorisation, the c- and affine directions
+    ph_fac<X, NX, NU>(ex, C);
+    if (ph_flag(ex, st, IS_OK)) ph_cpl<X, NX, NU>(ex, C);
+    if (ph_flag(ex, st, IS_OK)) ph_bkp<X, NX, NU>(ex, C);
+  } else if constexpr (G == 3) {
+    ph_refine<X, NX, NU, 0>(ex, C, it);   // `it` carries the round
+  } else if constexpr (G == 4) {   // affine step, combined direction
+    ph_aff<X, NX, NU>(ex, C);
+    ph_cmb<X, NX, NU>(ex, C);
+  } else if constexpr (G == 5) {
+    ph_refine<X, NX, NU, 1>(ex, C, it);
+  } else {
+    return ph_upd<X, NX, NU>(ex, C, it);
+  }
+  return true;
+}
+
+template <class M>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm_g(const PhArgs a) {
+  if ((int)blockIdx.x >= a.batch) return;
+  const int e = a.e0 + blockIdx.x;
+  const Plan& P = a.B->P;
+  const Layout& L = a.B->L;
+  double* ws = a.ws + L.stride * (size_t)e;
+  using X = DevExecT<M::kTransform, true>;
+  constexpr int NX = M::NX, NU = M::NU;
+  extern __shared__ double lds_dyn[];
+  const X ex = solver_exec<M::kTransform, true>(P, lds_dyn);
+  ipm_prelude<X, M>(ex, P, L, ws);
+  ipm_eco<X, M>(ex, P, L, ws);
+  Ctx C;
+  C.P = (CPlan*)&P;
+  C.L = (CLayout*)&L;
+  C.ws = (gdouble*)ws;
+  const gdouble* st = C.ws + L.ist;
+  ph_group<X, NX, NU, 0>(ex, C, 0);
+  const int maxit = P.desc.maxit;
+  if (ph_flag(ex, st, IS_ACTIVE))
+    for (int it = 0; it <= maxit; ++it) {
+      ph_group<X, NX, NU, 1>(ex, C, it);
+      if (it == maxit || !ph_flag(ex, st, IS_ACTIVE)) break;
+      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 2>(ex, C, it);
+      const int nref = __builtin_amdgcn_readfirstlane((int)st[IS_NREF]);
+      for (int r = 0; r < nref; ++r)
+        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 3>(ex, C, r);
+      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 4>(ex, C, it);
+      for (int r = 0; r < nref; ++r)
+        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 5>(ex, C, r);
+      if (!__builtin_amdgcn_readfirstlane((int)ph_group<X, NX, NU, 6>(ex, C, it))) break;
+    }
+  const IpmResult r = ph_result(st);
+  ipm_unpack<X, M>(ex, P, L, ws, r);
+  const int lane = threadIdx.x;
+  if (a.upred)
+    for (int i = lane; i < P.U * P.d; i += 64) a.upred[(size_t)e * P.U * P.d + i] = ws[L.upred + i];
+  if (a.xpred)
+    for (int i = lane; i < P.T * P.n; i += 64) a.xpred[(size_t)e * P.T * P.n + i] = ws[L.xpred + i];
+  if (a.bw)
+    for (int i = lane; i < P.nbranch - 1; i += 64) a.bw[(size_t)e * (P.nbranch - 1) + i] = ws[L.w + 1 + i];
+  if (lane == 0) {
+    if (a.J) a.J[e] = ws[L.sol + P.oJ];
+    if (a.status) a.status[e] = r.exit_flag;
+    if (a.iters) a.iters[e] = r.iters;
+  }
+}
+
 template <class M, int PH>
-hipError_t launch_ph(const SolveLaunch& s, const PhArgs& a, int it) {
+hipError_t launch_ph(const SolveLaunch& s, const PhArgs& a, int it, hipStream_t st) {
   if (s.lds_bytes > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_ph<M, PH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)s.lds_bytes);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((k_ph<M, PH>), dim3(a.batch), dim3(64), s.lds_bytes, s.stream, a, it);
+  hipLaunchKernelGGL((k_ph<M, PH>), dim3(a.batch), dim3(64), s.lds_bytes, st, a, it);
   return hipGetLastError();
 }
 
-// the whole IPM of one solve launch (after k_tree), host-driven over the iterations
+// the whole IPM of one solve launch (after k_tree on s.stream), host-driven over the iterations.
+// Mode 1 splits the batch into s.nsub sub-batches, each on a stream of its own: a phase kernel
+// waits for the slowest ego of its sub-batch, and the other sub-batches' kernels fill the gap
+// (the HIP streams map to separate hardware queues).
 template <class M>
 hipError_t launch_ipm_phased(const SolveLaunch& s) {
-  const PhArgs a{s.bundle, s.ws, s.upred, s.xpred, s.bw, s.J, s.status, s.iters, s.d_count, s.batch};
   hipError_t e;
-#define BMPC_PH(ph, it_)                               \
-  if ((e = launch_ph<M, ph>(s, a, it_)) != hipSuccess) \
+  if (s.ph_mode == 2) {   // one kernel, grouped out-of-line phases
+    const PhArgs a{s.bundle, s.ws, s.upred, s.xpred, s.bw, s.J, s.status, s.iters, s.d_count, 0, s.batch};
+    if (s.lds_bytes > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void*)k_ipm_g<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)s.lds_bytes)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(k_ipm_g<M>, dim3(a.batch), dim3(64), s.lds_bytes, s.stream, a);
+    return hipGetLastError();
+  }
+  const int ns = s.nsub < 1 ? 1 : s.nsub > kMaxSub ? kMaxSub : s.nsub;
+  const int per = (s.batch + ns - 1) / ns;
+  PhArgs a[kMaxSub];
+  hipStream_t st[kMaxSub];
+  bool live[kMaxSub];
+  int nsub = 0;
+  for (int i = 0; i < ns && i * per < s.batch; ++i, ++nsub) {
+    const int lo = i * per, hi = lo + per < s.batch ? lo + per : s.batch;
+    a[i] = PhArgs{s.bundle, s.ws, s.upred, s.xpred, s.bw, s.J, s.status, s.iters,
+                  s.d_count + (size_t)i * (s.maxit + 1), lo, hi - lo};
+    st[i] = ns == 1 ? s.stream : s.sub[i];
+    live[i] = true;
+  }
+#define BMPC_PH(ph, it_, i)                                    \
+  if ((e = launch_ph<M, ph>(s, a[i], it_, st[i])) != hipSuccess) \
     return e;
-  if ((e = hipMemsetAsync(s.d_count, 0, sizeof(int32_t) * (size_t)(s.maxit + 1), s.stream)) != hipSuccess) return e;
-  BMPC_PH(PH_INIT1, 0)
-  BMPC_PH(PH_INIT2, 0)
-  BMPC_PH(PH_INIT3, 0)
+  if ((e = hipMemsetAsync(s.d_count, 0, sizeof(int32_t) * (size_t)nsub * (s.maxit + 1), s.stream)) != hipSuccess)
+    return e;
+  if (ns > 1) {   // the sub-streams start after k_tree and the counter reset on s.stream
+    if ((e = hipEventRecord(s.sub_ev[kMaxSub], s.stream)) != hipSuccess) return e;
+    for (int i = 0; i < nsub; ++i)
+      if ((e = hipStreamWaitEvent(st[i], s.sub_ev[kMaxSub], 0)) != hipSuccess) return e;
+  }
+  for (int i = 0; i < nsub; ++i) {
+    BMPC_PH(PH_INIT1, 0, i)
+    BMPC_PH(PH_INIT2, 0, i)
+    BMPC_PH(PH_INIT3, 0, i)
+  }
   int next_check = BMPC_PH_FIRST;
   for (int it = 0; it <= s.maxit; ++it) {
-    BMPC_PH(PH_RES, it)
-    if (it == s.maxit) break;   // RES exits every ego at maxit
-    BMPC_PH(PH_FAC, it)
-    BMPC_PH(PH_CPL, it)
-    BMPC_PH(PH_BKP, it)
-    BMPC_PH(PH_RFP0, it)
-    BMPC_PH(PH_RFP1, it)
-    BMPC_PH(PH_AFF, it)
-    BMPC_PH(PH_CMB, it)
-    BMPC_PH(PH_RFC0, it)
-    BMPC_PH(PH_RFC1, it)
-    BMPC_PH(PH_UPD, it)
+    bool any = false;
+    for (int i = 0; i < nsub; ++i) {
+      if (!live[i]) continue;
+      any = true;
+      BMPC_PH(PH_RES, it, i)
+      if (it == s.maxit) continue;   // RES exits every ego at maxit
+      BMPC_PH(PH_FAC, it, i)
+      BMPC_PH(PH_CPL, it, i)
+      BMPC_PH(PH_BKP, it, i)
+      BMPC_PH(PH_RFP0, it, i)
+      BMPC_PH(PH_RFP1, it, i)
+      BMPC_PH(PH_AFF, it, i)
+      BMPC_PH(PH_CMB, it, i)
+      BMPC_PH(PH_RFC0, it, i)
+      BMPC_PH(PH_RFC1, it, i)
+      BMPC_PH(PH_UPD, it, i)
+    }
+    if (!any || it == s.maxit) break;
     if (it + 1 >= next_check) {
       next_check += BMPC_PH_CHECK;
-      if ((e = hipMemcpyAsync(s.h_count, s.d_count + it, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream)) != hipSuccess)
-        return e;
-      if ((e = hipStreamSynchronize(s.stream)) != hipSuccess) return e;
-      if (*s.h_count == 0) break;   // every ego has exited
+      for (int i = 0; i < nsub; ++i)
+        if (live[i] && (e = hipMemcpyAsync(s.h_count + i, a[i].count + it, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                           st[i])) != hipSuccess)
+          return e;
+      for (int i = 0; i < nsub; ++i) {
+        if (!live[i]) continue;
+        if ((e = hipStreamSynchronize(st[i])) != hipSuccess) return e;
+        if (s.h_count[i] == 0) live[i] = false;   // every ego of the sub-batch has exited
+      }
     }
   }
-  BMPC_PH(PH_FIN, 0)
+  for (int i = 0; i < nsub; ++i) {
+    BMPC_PH(PH_FIN, 0, i)
+    if (ns > 1) {   // s.stream resumes after every sub-batch
+      if ((e = hipEventRecord(s.sub_ev[i], st[i])) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(s.stream, s.sub_ev[i], 0)) != hipSuccess) return e;
+    }
+  }
 #undef BMPC_PH
   return hipSuccess;
 }

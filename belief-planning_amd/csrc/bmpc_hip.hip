@@ -19,6 +19,9 @@ using namespace bmpc::dev;
 #ifndef BMPC_IPM_PHASED_DEFAULT
 #define BMPC_IPM_PHASED_DEFAULT 0
 #endif
+#ifndef BMPC_PH_STREAMS_DEFAULT
+#define BMPC_PH_STREAMS_DEFAULT 4
+#endif
 
 namespace {
 
@@ -185,8 +188,10 @@ struct bmpc_plan {
   double t_acc[2] = {0, 0};
   int t_cnt = 0;
   bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
-  int32_t* d_count = nullptr;   // phase-per-kernel IPM: egos going on per iteration [maxit + 1]
-  int32_t* h_count = nullptr;   // ... its pinned read-back slot
+  int32_t* d_count = nullptr;   // phase-per-kernel IPM: egos going on per iteration [kMaxSub][maxit + 1]
+  int32_t* h_count = nullptr;   // ... pinned read-back slots [kMaxSub]
+  hipStream_t sub[kMaxSub] = {};   // ... its sub-batch streams
+  hipEvent_t sub_ev[kMaxSub + 1] = {};
 };
 
 extern "C" {
@@ -238,8 +243,8 @@ int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_
       hipMalloc(&pl->d_in, sizeof(double) * (size_t)batch * P.n * 3) != hipSuccess ||
       hipMalloc(&pl->d_out, sizeof(double) * (size_t)batch * ((size_t)P.U * P.d + (size_t)P.T * P.n + P.nbranch + 1)) != hipSuccess ||
       hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess ||
-      hipMalloc(&pl->d_count, sizeof(int32_t) * (size_t)(P.desc.maxit + 1)) != hipSuccess ||
-      hipHostMalloc(&pl->h_count, sizeof(int32_t)) != hipSuccess)
+      hipMalloc(&pl->d_count, sizeof(int32_t) * kMaxSub * (size_t)(P.desc.maxit + 1)) != hipSuccess ||
+      hipHostMalloc(&pl->h_count, sizeof(int32_t) * kMaxSub) != hipSuccess)
     return cleanup(fail(-12, "hipMalloc failed (out of device memory?)"));
   if (hipMemcpy(pl->d_tables, pl->hp.blob.data(), pl->hp.blob.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(-5, "hipMemcpy tables failed"));
@@ -261,6 +266,10 @@ int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_
     return cleanup(fail(-5, "hipStreamCreate failed"));
   for (auto& e : pl->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(-5, "hipEventCreate failed"));
+  for (auto& q : pl->sub)
+    if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(-5, "hipStreamCreate failed"));
+  for (auto& e : pl->sub_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return cleanup(fail(-5, "hipEventCreate failed"));
   *out = pl;
   return 0;
 }
@@ -280,6 +289,13 @@ int bmpc_plan_destroy(bmpc_plan* pl) {
   hipFree(pl->d_count);
   if (pl->h_count) hipHostFree(pl->h_count);
   for (auto& e : pl->ev)
+    if (e) hipEventDestroy(e);
+  for (auto& q : pl->sub)
+    if (q) {
+      hipStreamSynchronize(q);
+      hipStreamDestroy(q);
+    }
+  for (auto& e : pl->sub_ev)
     if (e) hipEventDestroy(e);
   if (pl->stream) hipStreamDestroy(pl->stream);
   delete pl;
@@ -375,9 +391,10 @@ static int fold_timing(bmpc_plan* pl) {
   return 0;
 }
 
-static bool use_phased() {
+// 0: monolithic k_ipm, 1: one kernel per IPM phase, 2: one kernel calling grouped phases (k_ipm_g)
+static int use_phased() {
   const char* e = getenv("BMPC_IPM_PHASED");
-  return e ? atoi(e) != 0 : BMPC_IPM_PHASED_DEFAULT;
+  return e ? atoi(e) : BMPC_IPM_PHASED_DEFAULT;
 }
 
 static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
@@ -413,7 +430,14 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   // the CVaR IPM runs phase per kernel (bmpc_dev_ph.h) when its plan's LDS-rich layout is the
   // launch's (the factored coupling system is re-read into LDS by each kernel that solves with it);
   // BMPC_IPM_PHASED=0 selects the monolithic k_ipm
-  if (phased && (P.desc.controller != BMPC_CTRL_CVAR || !tl || !use_phased())) phased = nullptr;
+  a.ph_mode = use_phased();
+  a.sub = pl->sub;
+  a.sub_ev = pl->sub_ev;
+  {   // sub-batch streams of the phase-per-kernel IPM (BMPC_PH_STREAMS; 1 = all on the solve's stream)
+    const char* e = getenv("BMPC_PH_STREAMS");
+    a.nsub = e ? atoi(e) : BMPC_PH_STREAMS_DEFAULT;
+  }
+  if (phased && (P.desc.controller != BMPC_CTRL_CVAR || !tl || a.ph_mode == 0)) phased = nullptr;
   if (phased) solver = phased;
   hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));

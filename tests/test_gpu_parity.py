@@ -4,7 +4,8 @@ Tolerances (stated per check):
 * model functions: 1e-12 relative -- same closed-form expressions, fp64;
 * solver: the reference solves with ECOS to feastol=abstol=reltol=1e-8 (MPC_branch.py:2136),
   so a solution is only defined to that precision.  J must agree to 1e-6 relative and the
-  applied input uPred[0] to 1e-4 absolute (|u| <= 6); the unique part of the primal vector
+  applied input uPred[0] to 1e-6 absolute on steps both sides end optimal (exit 0; 1e-4 against
+  the oracle's independent solves of the seeded batch, 5e-3 on "inaccurate" steps); the unique part of the primal vector
   (everything except the cost-free leaf-terminal slacks) to 1e-3 absolute.  GPU vs the
   host build of the same algorithm is compared tighter (J 1e-7 rel, uPred 1e-5 abs).
 """
