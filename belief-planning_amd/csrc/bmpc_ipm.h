@@ -1555,14 +1555,19 @@ BMPC_HD void bw_node(const X& ex, int gl, const double (&qx)[RX], const double (
 // eq-space (first T*n rows; Layout::zeros with es = 0 for none).  Solutions go to
 // o0 + i*os (z-space tree parts) and n0 + i*ns (eq-space multipliers; n0 = NULL skips).
 // Every vector lives in the ego's slab.
-// Structure: (1) lane-parallel pre-pass: slack elimination of every node's x rhs;
-// (2) the two sequential sweeps, one task per (branch, rhs) run by a group of
+// Structure: the two sequential sweeps, one task per (branch, rhs) run by a group of
 // W = X::kTaskLanes lanes (a DPP quad on the GPU; lane gl owns state rows gl*RX..), carrying
-// the affine term l / the state x in registers along the branch -- only the Riccati data
-// is loaded per node; (3) lane-parallel post-pass: multipliers nu and slack recovery.
+// the affine term l / the state x in registers along the branch.  Each node's slack
+// elimination (the x right-hand side qx0 = -r_x - sum_c f_c df r_S / sd) comes from a
+// lane-parallel pre-pass or, for plans whose staging does not fit LDS, is formed inside the
+// backward sweep from loads that do not depend on the recursion; a lane-parallel post-pass
+// forms the multipliers nu and recovers the slacks.
+// The first ncw right-hand sides are Woodbury cone columns (kkt_coupling): column k is
+// supported on cone k's child branch only, so its backward sweep runs only on that branch and
+// its ancestors (elsewhere l and kf are exactly zero and are not stored or read).
 template <class X, int NX, int NU>
 BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* r0, size_t rs, const gdouble* e0,
-                        size_t es, gdouble* o0, size_t os, gdouble* n0, size_t ns) {
+                        size_t es, gdouble* o0, size_t os, gdouble* n0, size_t ns, int ncw = 0) {
   const Ctx C = Cin.uniform();
   r0 = uniform_ptr(r0);
   e0 = uniform_ptr(e0);
@@ -1570,6 +1575,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   n0 = uniform_ptr(n0);
   constexpr int W = X::kTaskLanes;
   constexpr int RX = (NX + W - 1) / W;
+  constexpr int NCM = BMPC_MAX_FX + 1;   // LP rows per state node, compile-time bound
+  (void)NCM;
   CPlan& P = *C.P;
   CLayout& L = *C.L;
   BMPC_PROF(C.ws, L, PROF_TREESOLVE);
@@ -1578,24 +1585,49 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   const int Nc = P.Nc;
   gdouble* ws = C.ws;
   gdouble* lv_ = ws + L.lvec;   // [nr][T][NX]
-  gdouble* q0_ = ws + L.qx0;    // [nr][T][NX]
   gdouble* kf_ = ws + L.kff;    // [nr][U][NU]
   const size_t lstr = (size_t)P.T * NX, kstr = (size_t)P.U * NU;
-  const size_t roff = (size_t)(r0 - ws), eoff = (size_t)(e0 - ws);
   const gdouble* dh = ws + L.dh;
   const gdouble* sdv = ws + L.sd;
   const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
-
-  BMPC_TIC(t_pre);
-  // ---- (1) pre-pass: qx0 = -r_x - sum_c f_c df r_S / sd (non-terminal nodes) -------------
-  // two flat passes (the slack terms a_kc into LDS scratch, then the node sums): a loop
-  // over c with loads inside would cost one round trip per c
-  ldouble* av = ex.lds + P.lds_scr;
-  const bool av_lds = P.nscr >= P.T * Nc;
-  for (int ri = 0; ri < nr; ++ri) {
-    const gdouble* rr = r0 + ri * rs;
-    gdouble* q0 = q0_ + ri * lstr;
-    if (av_lds) {
+  // rhs ri needs the backward sweep on branch b (see above)
+  auto needed = [&](int b, int ri) {
+    if (ri >= ncw) return true;
+    int c = t.cone_c[ri];
+    if (c < 0) return b == 0;   // the root cone: the root node
+    while (c > b) c = (c - 1) / P.m;
+    return c == b;
+  };
+  // the x right-hand side of row i of node k after slack elimination (qx0), all loads issued
+  // together: -r_x + dh a_0 - sum_{c>=1} Fx[c-1] a_c, a_c = [k non-terminal] df_c r_S,c / sd_c
+  auto qx0 = [&](const gdouble* rr, int k, int i) {
+    double rS[NCM], s0[NCM], s1[NCM];
+#pragma unroll
+    for (int c = 0; c < NCM; ++c) {
+      const int kc = k * Nc + (c < Nc ? c : 0);
+      rS[c] = rr[P.oS + kc];
+      s0[c] = sdv[kc * 2];
+      s1[c] = sdv[kc * 2 + 1];
+    }
+    const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // terminal nodes add 0
+    double v = -rr[P.oX + k * NX + i] + dh[k * NX + i] * (on * s1[0] * rS[0] / s0[0]);
+#pragma unroll
+    for (int c = 1; c < NCM; ++c)
+      if (c < Nc) v -= fxv(P, ex, c - 1, i) * (on * s1[c] * rS[c] / s0[c]);
+    return v;
+  };
+  // plans whose slack terms fit the LDS staging area (Plan::nscr) form the x right-hand sides
+  // in a lane-parallel pre-pass (two flat passes per rhs: the slack terms a_kc into LDS, then
+  // the node sums); the others form them inside the backward sweep (qx0 above) -- measured:
+  // the N=20 NB=1 plan is 2% faster with the pre-pass, N=8 NB=2 5% faster without
+  const bool pre = ex.uniform(P.nscr >= P.T * Nc);
+  gdouble* q0_ = ws + L.qx0;    // [nr][T][NX] (pre-pass plans)
+  if (pre) {
+    BMPC_TIC(t_pre);
+    ldouble* av = ex.lds + P.lds_scr;
+    for (int ri = 0; ri < nr; ++ri) {
+      const gdouble* rr = r0 + ri * rs;
+      gdouble* q0 = q0_ + ri * lstr;
       lane_batch<BMPC_TS_UN_AV>(ex, 0, P.T * Nc, [&](int it) {
         const int k = it / Nc;
         const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // terminal nodes add 0
@@ -1609,39 +1641,55 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         return v;
       }, [&](int it, double v) { q0[it] = v; });
       ex.sync();
-    } else {
-      lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
-        const int k = it / NX, j = it % NX;
-        const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
-        double v = -rr[P.oX + it];
-        for (int c = 0; c < Nc; ++c) {
-          const double a = sdv[(k * Nc + c) * 2 + 1] * rr[P.oS + k * Nc + c] / sdv[(k * Nc + c) * 2];
-          const double dhv = dh[it], fx = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
-          v -= on * (m0 * (-dhv) + (1.0 - m0) * fx) * a;
-        }
-        return v;
-      }, [&](int it, double v) { q0[it] = v; });
     }
+    BMPC_TOC(C.ws, L, PROF_X1, t_pre);
   }
-  ex.sync();
 
-  BMPC_TOC(C.ws, L, PROF_X1, t_pre);
   BMPC_TIC(t_bw);
-  // ---- (2a) backward sweep (leaves -> root) ----------------------------------------------
+  // ---- backward sweep (leaves -> root) -------------------------------------------------------
   // The per-node loads do not depend on the recursion: one memory round trip per node.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
-    const int ntask = nbd * nr;
+    // the needed tasks of this depth, in order: first the (branch, rhs >= ncw) pairs, then for
+    // every cone column the branch of its root path at this depth
+    const int nfull = nbd * (nr - ncw);
+    int ncol = 0;
+    for (int ri = 0; ri < ncw; ++ri) {
+      const int c = t.cone_c[ri];
+      ncol += (c < 0 ? 0 : t.br_depth[c]) >= dep ? 1 : 0;
+    }
+    const int ntask = nfull + ncol;
     const int rounds = (ntask + ngrp - 1) / ngrp;
     const bool leaf = dep == P.NB;
     for (int rd = 0; rd < rounds; ++rd) {
       const int task = rd * ngrp + grp;
       if (task >= ntask) continue;       // whole group idle together
-      const int b = b0 + task / nr, ri = task % nr;
+      int b, ri;
+      if (task < nfull) {
+        b = b0 + task / (nr - ncw);
+        ri = ncw + task % (nr - ncw);
+      } else {
+        int want = task - nfull;
+        ri = 0;
+        for (int r2 = 0; r2 < ncw; ++r2) {
+          const int c = t.cone_c[r2];
+          if ((c < 0 ? 0 : t.br_depth[c]) >= dep) {
+            if (want == 0) {
+              ri = r2;
+              break;
+            }
+            --want;
+          }
+        }
+        int c = t.cone_c[ri];
+        if (c < 0) c = 0;
+        while (t.br_depth[c] > dep) c = (c - 1) / P.m;
+        b = c;
+      }
       const gdouble* rr = r0 + ri * rs;
       const gdouble* ee = e0 + ri * es;
-      gdouble* lvec = lv_ + ri * lstr;
       const gdouble* q0 = q0_ + ri * lstr;
+      gdouble* lvec = lv_ + ri * lstr;
       gdouble* kf = kf_ + ri * kstr;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const int c0 = t.br_child0[b];
@@ -1651,7 +1699,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q;
-          l[q] = i < NX ? q0[tn * NX + i] : 0.0;
+          l[q] = i < NX ? (pre ? q0[tn * NX + i] : qx0(rr, tn, i)) : 0.0;
           if (i < NX) lvec[tn * NX + i] = l[q];
         }
       }
@@ -1661,7 +1709,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
-          qx[q] = q0[k * NX + i];
+          qx[q] = pre ? q0[k * NX + i] : qx0(rr, k, i);
 #pragma unroll
           for (int j = 0; j < NX; ++j) Acol[q][j] = ws[L.Ad + u * NX * NX + j * NX + i];
 #pragma unroll
@@ -1689,6 +1737,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 #pragma unroll
           for (int q = 0; q < RX; ++q) g[q] = 0.0;
           for (int ci = 0; ci < P.m; ++ci) {
+            if (!needed(c0 + ci, ri)) continue;   // l = 0 and e = 0 there: adds exactly 0
             const int c = t.br_ndx[c0 + ci];
             double ec[NX];
 #pragma unroll
@@ -1719,7 +1768,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   }
   BMPC_TOC(C.ws, L, PROF_X2, t_bw);
   BMPC_TIC(t_fw);
-  // ---- (2b) forward sweep (root -> leaves): x and u only ------------------------------------
+  // ---- forward sweep (root -> leaves): x, u, and each node's multipliers and slacks ----------
   for (int it = ex.lane; it < nr * NX; it += ex.nlanes) {
     const int ri = it / NX, j = it % NX;
     o0[ri * os + P.oX + j] = e0[ri * es + j];
@@ -1737,6 +1786,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       gdouble* o = o0 + ri * os;
       const gdouble* ee = e0 + ri * es;
       const gdouble* kf = kf_ + ri * kstr;
+      const bool kfon = needed(b, ri);   // kf = 0 where the backward sweep was skipped
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const int c0 = t.br_child0[b];
       double xk[NX];      // full state (every lane of the group holds all of it)
@@ -1759,7 +1809,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
           en[q] = ee[kn * NX + i];
         }
 #pragma unroll
-        for (int m = 0; m < NU; ++m) kfu[m] = kf[u * NU + m];
+        for (int m = 0; m < NU; ++m) kfu[m] = kfon ? kf[u * NU + m] : 0.0;
         // ---- u = kf + K x ----
         double uk[NU];
 #pragma unroll
@@ -1805,19 +1855,19 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     }
     ex.sync();
   }
-
   BMPC_TOC(C.ws, L, PROF_X3, t_fw);
   BMPC_TIC(t_post);
-  // ---- (3) post-pass: nu_k = -(l_k + P_k x_k), slack recovery --------------------------------
+  // ---- post-pass: nu_k = -(l_k + P_k x_k), slack recovery -----------------------------------
   for (int ri = 0; ri < nr; ++ri) {
     gdouble* o = o0 + ri * os;
     const gdouble* rr = r0 + ri * rs;
     const gdouble* lvec = lv_ + ri * lstr;
     if (n0) {
       gdouble* nn = n0 + ri * ns;
+      const bool lon = ex.uniform(ri >= ncw);   // Woodbury columns: l = 0 off the column's root path
       lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
-        double v = lvec[it];
+        double v = (lon || needed(t.x_branch[k], ri)) ? lvec[it] : 0.0;
 #pragma unroll
         for (int j = 0; j < NX; ++j) v += ws[L.P + k * NX * NX + i * NX + j] * o[P.oX + k * NX + j];
         return -v;
@@ -1923,7 +1973,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   gdouble* ws = C.ws;
   const int nc = P.ncones;
   tree_solve<X, NX, NU>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv, ws + L.colnu,
-                        P.neq);
+                        P.neq, nc);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
   auto* M = coup_mem(ex, ws, L, P, P.lds_M);
   const gdouble* eta = ws + L.eta;

@@ -319,6 +319,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.lds_fu = P.lds_fx + P.nFx * n;
   P.nconst = P.lds_fu + P.nFu * d;
   P.lds_scr = std::max(64, (P.nconst + 7) & ~7);
+  // (plans whose staging does not fit form each node's slack terms inside the tree solve's sweep)
   P.nscr = desc.controller == BMPC_CTRL_CVAR && P.lds_scr + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
   P.lds_M = P.lds_scr + P.nscr;
   P.lds_piv = P.lds_M + P.nsm * P.nsm;
@@ -431,7 +432,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   const size_t nrhs = nc > 0 ? (size_t)nc + 2 : 1;
   L.kff = take(nrhs * U * d);
   L.lvec = take(nrhs * T * n);
-  L.qx0 = take(nrhs * T * n);   // slack-eliminated x rhs of the tree sweeps
+  L.qx0 = take(nrhs * T * n);   // slack-eliminated x rhs of the tree sweeps (pre-pass plans)
   if (nc > 0) {
     // contiguous rhs / solution blocks of the merged tree solve, stride nv (z-space) / neq
     // (eq-space): g_1..g_nc | tz_c | tz_a,  col_1..col_nc | x1 | x2,  colnu_1..nc | y1 | y2,
