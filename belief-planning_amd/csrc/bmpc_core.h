@@ -338,10 +338,21 @@ BMPC_HD double lane_sum(const X& ex, int lo, int hi, F f) {
 struct ConeGroups {
   int cg, ngrp, g, gl, rounds;
 };
+// lanes per cone group of an executor: 1 on the host, the plan's cgrp on one wave (cgrp *
+// ncones <= 64), and on a multi-wave executor the largest power of two <= 64 that still gives
+// every cone a group of its own
+template <class X>
+BMPC_HD int exec_cgrp(const X& ex, int cgrp, int ncones) {
+  if (ex.nlanes == 1) return 1;
+  if (ex.nlanes <= 64) return cgrp;
+  int cg = 64;
+  while (cg > 1 && cg * ncones > ex.nlanes) cg >>= 1;
+  return cg;
+}
 template <class X>
 BMPC_HD ConeGroups cone_groups(const X& ex, int cgrp, int ncones) {
   ConeGroups G;
-  G.cg = ex.nlanes == 1 ? 1 : cgrp;
+  G.cg = exec_cgrp(ex, cgrp, ncones);
   G.ngrp = ex.nlanes / G.cg;
   G.g = ex.lane / G.cg;
   G.gl = ex.lane % G.cg;

@@ -89,9 +89,90 @@ struct DevExecT {
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
     return v;
   }
+  // K sums at once (in place)
+  template <int K>
+  __device__ void sum_n(double* v) const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = sum(v[k]);
+  }
 };
 
 using DevExec = DevExecT<false>;
+
+// Multi-wave executor: one ego on NW waves of one workgroup (batch-1 / small-batch callers --
+// main_branch's one solve per step): the same phase templates with 64*NW lanes, so the tree
+// solve's tasks, the cone groups and every lane loop spread over NW waves.  Wave-level
+// operations (DPP quads, cone-group shuffles) are unchanged; whole-executor reductions go
+// through LDS (`red`, K*NW doubles) between two barriers.
+template <bool TR, bool TL, int NW>
+struct DevBlockExecT {
+  static constexpr bool kTransform = TR;
+  static constexpr bool kCoupLds = TL;
+  using tab_ptr = typename std::conditional<TL, lint*, gint*>::type;
+  int lane;
+  ldouble* lds;
+  tab_ptr tab;
+  ldouble* eco;
+  ldouble* red;   // reduction scratch: kRedMax * NW doubles
+  static constexpr int nlanes = 64 * NW;
+  static constexpr int kTaskLanes = 4;
+  static constexpr int kConeRegRows = 8;
+  static constexpr int kRedMax = 16;
+  __device__ double tsum(double v) const {
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    return v;
+  }
+  template <int S>
+  __device__ double tget(double v) const { return dpp_d<S | (S << 2) | (S << 4) | (S << 6)>(v); }
+  __device__ double gsum(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ double gmax(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ double gmin(double v, int g) const {
+    for (int o = g >> 1; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ void sync() const { __syncthreads(); }
+  __device__ bool uniform(bool b) const { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
+  // OP 0 sum, 1 max, 2 min of K values per lane over all lanes (in place)
+  template <int OP, int K>
+  __device__ void reduce(double* v) const {
+    static_assert(K <= kRedMax, "reduction scratch");
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double w = __shfl_xor(v[k], o, 64);
+        v[k] = OP == 0 ? v[k] + w : OP == 1 ? fmax(v[k], w) : fmin(v[k], w);
+      }
+    const int wv = lane >> 6;
+    __syncthreads();   // the previous reduction's readers are done with red
+    if ((lane & 63) == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[k * NW + wv] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double a = red[k * NW];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        const double b = red[k * NW + w];
+        a = OP == 0 ? a + b : OP == 1 ? fmax(a, b) : fmin(a, b);
+      }
+      v[k] = a;
+    }
+  }
+  __device__ double sum(double v) const { reduce<0, 1>(&v); return v; }
+  __device__ double max(double v) const { reduce<1, 1>(&v); return v; }
+  __device__ double min(double v) const { reduce<2, 1>(&v); return v; }
+  template <int K>
+  __device__ void sum_n(double* v) const { reduce<0, K>(v); }
+};
 
 constexpr int kMaxSub = 8;   // sub-batch streams of the phase-per-kernel IPM
 
@@ -125,6 +206,61 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
   } else {
     __syncthreads();
     return DevExecT<TR, TL>{(int)threadIdx.x, (ldouble*)lds_dyn, (gint*)gtab, (ldouble*)eco};
+  }
+}
+
+#ifndef BMPC_BLK_WAVES
+#define BMPC_BLK_WAVES 16   // waves per ego of the small-batch solver kernels (k_solve_blk)
+#endif
+
+// LDS of a multi-wave solver launch: the wave launch's, then the reduction scratch
+__host__ __device__ inline size_t solver_lds_bytes_blk(const Plan& P, bool transform, int nw) {
+  return ((solver_lds_bytes(P, transform, true) + 7) & ~(size_t)7) + sizeof(double) * 16 * (size_t)nw;
+}
+template <bool TR, int NW>
+__device__ __forceinline__ DevBlockExecT<TR, true, NW> solver_exec_blk(const Plan& P, double* lds_dyn) {
+  const int t = threadIdx.x, nt = 64 * NW;
+  for (int i = t; i < P.nconst; i += nt) lds_dyn[P.lds_w + i] = plan_const(P, i);
+  const int32_t* gtab = (const int32_t*)P.t.br_depth;
+  int32_t* tabl = reinterpret_cast<int32_t*>(lds_dyn + P.nlds);
+  for (int i = t; i < P.ntab; i += nt) tabl[i] = gtab[i];
+  double* eco = lds_dyn + (solver_lds_bytes(P, false, true) / sizeof(double));
+  double* red = lds_dyn + ((solver_lds_bytes(P, TR, true) + 7) & ~(size_t)7) / sizeof(double);
+  __syncthreads();
+  return DevBlockExecT<TR, true, NW>{t, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco, (ldouble*)red};
+}
+
+// One ego per workgroup of NW waves (small batches: every wave of the chip on few egos);
+// QP: the OSQP-class controllers' k_qp path, else the CVaR IPM.
+template <class M, bool QP, int NW>
+__global__ __launch_bounds__(64 * NW) void k_solve_blk(const Bundle* __restrict__ B, double* __restrict__ ws,
+                                                      const bmpc_policy* __restrict__ pol, double* upred,
+                                                      double* xpred, double* bw, double* J, int32_t* status,
+                                                      int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  constexpr bool TR = QP ? false : M::kTransform;
+  extern __shared__ double lds_dyn[];
+  const auto ex = solver_exec_blk<TR, NW>(P, lds_dyn);
+  using X = DevBlockExecT<TR, true, NW>;
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r;
+  if constexpr (QP) r = solve_ego_qp<X, M>(ex, P, L, E);
+  else r = solve_ego_ipm<X, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x, nt = 64 * NW;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += nt) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += nt) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += nt) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = QP ? r.pcost : w[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
   }
 }
 
@@ -251,6 +387,27 @@ hipError_t launch_solver(const SolveLaunch& a) {
   return a.rich ? launch_solver_kernel(k_ipm<M, true>, a) : launch_solver_kernel(k_ipm<M, false>, a);
 }
 
+// the small-batch launch: one ego per NW-wave workgroup (solver_lds_bytes_blk of LDS)
+template <class M, bool QP>
+hipError_t launch_blk_kernel(const SolveLaunch& a) {
+  constexpr int NW = BMPC_BLK_WAVES;
+  if (a.lds_bytes > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_solve_blk<M, QP, NW>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((k_solve_blk<M, QP, NW>), dim3(a.batch), dim3(64 * NW), a.lds_bytes, a.stream, a.bundle, a.ws,
+                     a.pol, a.upred, a.xpred, a.bw, a.J, a.status, a.iters, a.batch);
+  return hipGetLastError();
+}
+template <class M, bool WITH_QP>
+hipError_t launch_solver_blk(const SolveLaunch& a) {
+  if constexpr (WITH_QP) {
+    if (a.qp) return launch_blk_kernel<M, true>(a);
+  }
+  return launch_blk_kernel<M, false>(a);
+}
+
 // the per-model launchers (bmpc_k_highway.hip, bmpc_k_highway_t.hip, bmpc_k_merge.hip,
 // bmpc_k_quadruped.hip)
 hipError_t launch_tree_highway(const SolveLaunch& a);
@@ -261,6 +418,10 @@ hipError_t launch_tree_merge(const SolveLaunch& a);
 hipError_t launch_solver_merge(const SolveLaunch& a);
 hipError_t launch_tree_quadruped(const SolveLaunch& a);
 hipError_t launch_solver_quadruped(const SolveLaunch& a);
+hipError_t launch_solver_blk_highway(const SolveLaunch& a);
+hipError_t launch_solver_blk_highway_t(const SolveLaunch& a);
+hipError_t launch_solver_blk_merge(const SolveLaunch& a);
+hipError_t launch_solver_blk_quadruped(const SolveLaunch& a);
 // the phase-per-kernel CVaR IPM (bmpc_kp_*.hip)
 hipError_t launch_ipm_phased_highway(const SolveLaunch& a);
 hipError_t launch_ipm_phased_highway_t(const SolveLaunch& a);

@@ -430,6 +430,19 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   // the CVaR IPM runs phase per kernel (bmpc_dev_ph.h) when its plan's LDS-rich layout is the
   // launch's (the factored coupling system is re-read into LDS by each kernel that solves with it);
   // BMPC_IPM_PHASED=0 selects the monolithic k_ipm
+  // small batches: one ego per 16-wave workgroup (BMPC_BLOCK_EGOS: the largest batch that takes
+  // this path; default one ego per CU)
+  int blk_max = pl->ctx->cus;
+  if (const char* e = getenv("BMPC_BLOCK_EGOS")) blk_max = atoi(e);
+  const bool blk = B <= blk_max;
+  if (blk) {
+    a.lds_bytes = solver_lds_bytes_blk(P, xform, BMPC_BLK_WAVES);
+    a.rich = true;
+    if (hwt) solver = launch_solver_blk_highway_t;
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY) solver = launch_solver_blk_highway;
+    else if (merge) solver = launch_solver_blk_merge;
+    else solver = launch_solver_blk_quadruped;
+  }
   a.ph_mode = use_phased();
   a.sub = pl->sub;
   a.sub_ev = pl->sub_ev;
@@ -437,7 +450,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     const char* e = getenv("BMPC_PH_STREAMS");
     a.nsub = e ? atoi(e) : BMPC_PH_STREAMS_DEFAULT;
   }
-  if (phased && (P.desc.controller != BMPC_CTRL_CVAR || !tl || a.ph_mode == 0)) phased = nullptr;
+  if (phased && (blk || P.desc.controller != BMPC_CTRL_CVAR || !tl || a.ph_mode == 0)) phased = nullptr;
   if (phased) solver = phased;
   hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));

@@ -136,11 +136,7 @@ BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] += av[a] * bv[b];
   }
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      if (a < na && b < nb) acc[a][b] = ex.sum(acc[a][b]);
+  ex.template sum_n<16>(&acc[0][0]);   // all sixteen in one reduction (one barrier pair on a multi-wave executor)
 }
 
 // ------------------------------------------------------------------------------------
@@ -204,8 +200,7 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
 // Plans whose largest cone does not fit (P.maxq > kConeRegRows * cg) run the unfused chain.
 template <class X>
 BMPC_HD bool cone_regs(const X& ex, CPlan& P) {
-  const int cg = ex.nlanes == 1 ? 1 : P.cgrp;
-  return P.maxq <= X::kConeRegRows * cg;
+  return P.maxq <= X::kConeRegRows * exec_cgrp(ex, P.cgrp, P.ncones);
 }
 
 // y = sc (2 a (a'v) - J v) over one cone's register rows (rows past q hold a = v = 0);

@@ -49,6 +49,8 @@ struct HostExecT {
   double sum(double v) const { return v; }
   double max(double v) const { return v; }
   double min(double v) const { return v; }
+  template <int K>
+  void sum_n(double*) const {}
 };
 using HostExec = HostExecT<false>;
 
