@@ -19,6 +19,9 @@ using namespace bmpc::dev;
 #ifndef BMPC_IPM_PHASED_DEFAULT
 #define BMPC_IPM_PHASED_DEFAULT 0
 #endif
+#ifndef BMPC_BLOCK_MIN_T
+#define BMPC_BLOCK_MIN_T 256   // state nodes of the smallest tree that takes the multi-wave small-batch path
+#endif
 #ifndef BMPC_PH_STREAMS_DEFAULT
 #define BMPC_PH_STREAMS_DEFAULT 4
 #endif
@@ -427,14 +430,15 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t, phased = launch_ipm_phased_highway_t;
   else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway, phased = launch_ipm_phased_highway;
   else if (merge) tree = launch_tree_merge, solver = launch_solver_merge, phased = launch_ipm_phased_merge;
-  // the CVaR IPM runs phase per kernel (bmpc_dev_ph.h) when its plan's LDS-rich layout is the
-  // launch's (the factored coupling system is re-read into LDS by each kernel that solves with it);
-  // BMPC_IPM_PHASED=0 selects the monolithic k_ipm
-  // small batches: one ego per 16-wave workgroup (BMPC_BLOCK_EGOS: the largest batch that takes
-  // this path; default one ego per CU)
+  // Small batches of large CVaR trees: one ego per 16-wave workgroup (k_solve_blk) when the
+  // batch leaves CUs idle.  Measured at one ego: N=30 NB=2 69-78 ms vs 105-109 ms on one wave;
+  // N=8 NB=2 41-47 vs 34-39 ms and N=20 NB=1 21-23 vs 15-17 ms (the extra barriers of the
+  // workgroup-wide reductions cost more than the wider loops save), hence the T threshold.
+  // BMPC_BLOCK_EGOS: the largest batch that takes this path (default: one ego per CU).
   int blk_max = pl->ctx->cus;
   if (const char* e = getenv("BMPC_BLOCK_EGOS")) blk_max = atoi(e);
-  const bool blk = B <= blk_max;
+  const bool blk = B <= blk_max && P.desc.controller == BMPC_CTRL_CVAR &&
+                   (P.T >= BMPC_BLOCK_MIN_T || getenv("BMPC_BLOCK_EGOS"));
   if (blk) {
     a.lds_bytes = solver_lds_bytes_blk(P, xform, BMPC_BLK_WAVES);
     a.rich = true;
@@ -443,6 +447,9 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     else if (merge) solver = launch_solver_blk_merge;
     else solver = launch_solver_blk_quadruped;
   }
+  // large batches of the CVaR IPM: the monolithic k_ipm (mode 0), one kernel per phase
+  // (bmpc_dev_ph.h, mode 1: the factored coupling system re-read into LDS by every kernel that
+  // solves with it) or one kernel calling grouped phase functions (mode 2); BMPC_IPM_PHASED
   a.ph_mode = use_phased();
   a.sub = pl->sub;
   a.sub_ev = pl->sub_ev;

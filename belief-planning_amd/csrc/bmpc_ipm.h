@@ -140,6 +140,83 @@ BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const
 }
 
 // ------------------------------------------------------------------------------------
+// Cone k's rank-1 vector g_k = G_k'(J wbar) is zero outside its support among the tree
+// variables: the x / u / S entries of its child branch's N nodes (the root cone: the root
+// node's u and S).  Plans with many cones (NB = 2: 13, each supported on 1/13 of the tree) form
+// the coupling products over the support only; the N = 20 NB = 1 plan's 4 cones cover a third
+// each, and there one pass over all tree variables is faster (block_dots).
+// ------------------------------------------------------------------------------------
+template <class T>
+BMPC_HD int cone_supp_len(CPlan& P, const T& t, int k) {
+  return t.cone_c[k] >= 0 ? P.N * (P.n + P.d + P.Nc) : P.d + P.Nc;
+}
+// index (into the primal vector) of entry e of cone k's support
+template <class T>
+BMPC_HD int cone_supp_idx(CPlan& P, const T& t, int k, int e) {
+  const int c = t.cone_c[k];
+  if (c < 0) return e < P.d ? P.oU + e : P.oS + (e - P.d);
+  const int xn = P.N * P.n, un = P.N * P.d;
+  if (e < xn) return P.oX + t.br_ndx[c] * P.n + e;
+  if (e < xn + un) return P.oU + t.br_ndu[c] * P.d + (e - xn);
+  return P.oS + t.br_ndx[c] * P.Nc + (e - xn - un);
+}
+BMPC_HD bool coup_supp_dots(CPlan& P) { return P.ncones > 4; }
+
+// acc[j] = g_k' v_{j0 + j} over cone k's support (j < 16, j0 + j < nvec; v_j = v0 + j * vstr)
+template <class X, class T>
+BMPC_HD void cone_supp_dots(const X& ex, CPlan& P, const T& t, const gdouble* gk, int k, const gdouble* v0,
+                            size_t vstr, int j0, int nvec, double (&acc)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+  const int tot = cone_supp_len(P, t, k);
+  for (int e = ex.lane; e < tot; e += ex.nlanes) {
+    const int i = cone_supp_idx(P, t, k, e);
+    const double g = gk[i];
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = v0[(size_t)(j0 + j < nvec ? j0 + j : j0) * vstr + i];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += (j0 + j < nvec ? g : 0.0) * v[j];
+  }
+  ex.template sum_n<16>(acc);
+}
+
+// acc[k] = g_k' dx over each cone's support, all cones in one batched pass (k < 16 per call:
+// cones k0 .. k0 + 15)
+template <class X, class T>
+BMPC_HD void cone_supp_gdx(const X& ex, CPlan& P, const T& t, const gdouble* g0, size_t gstr, const gdouble* dx, int k0,
+                           double (&acc)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+  const int nc = P.ncones;
+  const int kn = nc - k0 < 16 ? nc - k0 : 16;
+  const int full = P.N * (P.n + P.d + P.Nc);   // support length of every non-root cone
+  // flattened (cone, entry) index: cones k0.. in order, the root cone (last) shorter
+  int tot = 0;
+  for (int j = 0; j < kn; ++j) tot += cone_supp_len(P, t, k0 + j);
+  constexpr int UN = 8;
+  for (int b = ex.lane; b < tot; b += UN * ex.nlanes) {
+    double gv[UN], xv[UN];
+    int kk[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int f = b + u * ex.nlanes < tot ? b + u * ex.nlanes : b;
+      const int j = f / full < kn ? f / full : kn - 1;
+      const int e = f - j * full;
+      const int i = cone_supp_idx(P, t, k0 + j, e);
+      kk[u] = b + u * ex.nlanes < tot ? j : -1;
+      gv[u] = g0[(size_t)(k0 + j) * gstr + i];
+      xv[u] = dx[i];
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] += (kk[u] == j ? gv[u] : 0.0) * xv[u];
+  }
+  ex.template sum_n<16>(acc);
+}
+
+// ------------------------------------------------------------------------------------
 // reductions over one cone's rows, by the cone group G that owns the cone (k >= 0) or as an
 // idle member (k < 0, q = 0): every lane of the wave must make the same calls.
 // ------------------------------------------------------------------------------------
@@ -1977,24 +2054,37 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   const int ntree = P.oRho;    // x and u parts are [0, oRho); S part [oS, oJ)
   for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
   ex.sync();
-  // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables,
-  // 4 x 4 blocks of dot products per pass
-  for (int k0 = 0; k0 < nc; k0 += 4)
-    for (int j0 = 0; j0 < nc; j0 += 4) {
-      const int na = nc - k0 < 4 ? nc - k0 : 4, nbk = nc - j0 < 4 ? nc - j0 : 4;
-      double acc[4][4];
-      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, ws + L.colk + (size_t)j0 * P.nv, P.nv, nbk,
-                 0, ntree, P.oS, P.oJ, acc);
-      if (ex.lane == 0)
-        for (int a = 0; a < na; ++a) {
-          const int k = k0 + a;
+  // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables
+  if (coup_supp_dots(P)) {   // many cones: over each g_k's support, 16 columns per pass
+    const auto t = topo_view(P, ex);
+    for (int k = 0; k < nc; ++k)
+      for (int j0 = 0; j0 < nc; j0 += 16) {
+        double acc[16];
+        cone_supp_dots(ex, P, t, ws + L.gk + (size_t)k * P.nv, k, ws + L.colk, P.nv, j0, nc, acc);
+        if (ex.lane == 0) {
           const double ck = 2.0 / (eta[k] * eta[k]);
-          for (int b = 0; b < nbk; ++b) {
-            const int j = j0 + b;
-            M[(ng + nb + k) * ns + ng + nb + j] = ck * acc[a][b] + (k == j ? 1.0 : 0.0);
-          }
+          for (int j = j0; j < nc && j < j0 + 16; ++j)
+            M[(ng + nb + k) * ns + ng + nb + j] = ck * acc[j - j0] + (k == j ? 1.0 : 0.0);
         }
-    }
+      }
+  } else {   // 4 x 4 blocks of dot products per pass over all tree variables
+    for (int k0 = 0; k0 < nc; k0 += 4)
+      for (int j0 = 0; j0 < nc; j0 += 4) {
+        const int na = nc - k0 < 4 ? nc - k0 : 4, nbk = nc - j0 < 4 ? nc - j0 : 4;
+        double acc[4][4];
+        block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, ws + L.colk + (size_t)j0 * P.nv, P.nv, nbk,
+                   0, ntree, P.oS, P.oJ, acc);
+        if (ex.lane == 0)
+          for (int a = 0; a < na; ++a) {
+            const int k = k0 + a;
+            const double ck = 2.0 / (eta[k] * eta[k]);
+            for (int b = 0; b < nbk; ++b) {
+              const int j = j0 + b;
+              M[(ng + nb + k) * ns + ng + nb + j] = ck * acc[a][b] + (k == j ? 1.0 : 0.0);
+            }
+          }
+      }
+  }
   // H_gg diagonal: LP rows -rho, -mu+, -mu-
   for (int b = ex.lane; b < nb; b += ex.nlanes) {
     const double w = dl[P.rRisk + b];
@@ -2071,12 +2161,22 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
   auto* b = coup_mem(ex, ws, L, P, P.lds_rhs);
   const gdouble* eta = ws + L.eta;
-  for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
-    const int na = nc - k0 < 4 ? nc - k0 : 4;
-    double acc[4][4];
-    block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
-    if (ex.lane == 0)
-      for (int a = 0; a < na; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
+  if (coup_supp_dots(P)) {   // g_k' dx over each cone's support, sixteen cones per pass
+    const auto t = topo_view(P, ex);
+    for (int k0 = 0; k0 < nc; k0 += 16) {
+      double acc[16];
+      cone_supp_gdx(ex, P, t, ws + L.gk, P.nv, dx, k0, acc);
+      if (ex.lane == 0)
+        for (int a = 0; a < 16 && k0 + a < nc; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a];
+    }
+  } else {
+    for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
+      const int na = nc - k0 < 4 ? nc - k0 : 4;
+      double acc[4][4];
+      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
+      if (ex.lane == 0)
+        for (int a = 0; a < na; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
+    }
   }
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();

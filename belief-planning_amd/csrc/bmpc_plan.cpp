@@ -286,6 +286,10 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.nrows = row;
   P.maxq = 0;
   for (int q : hp.cone_q) P.maxq = q > P.maxq ? q : P.maxq;
+  // widen the cone groups (more rounds) until the widest cone fits the fused cone passes'
+  // registers, 8 rows per lane (bmpc_ipm.h cone_regs): NB = 2 plans' 13 cones of 2 + N (n + d)
+  // rows otherwise run the unfused chain of whole-vector passes
+  while (P.cgrp < 64 && P.maxq > 8 * P.cgrp) P.cgrp <<= 1;
   if (desc.controller != BMPC_CTRL_CVAR) {
     // BranchMPCProx's / BranchMPC's OSQP vector z = [X | U | S] and rows [Fx-type | Fu | -S] (MPC_branch.py:185-370)
     P.oS = T * n + U * d;
