@@ -1399,6 +1399,17 @@ BMPC_HD bool riccati_step(const double (&Hx)[NX][NX], const double (&Hu)[NU][NU]
   return ok;
 }
 
+// all NX entries of a row-distributed vector (lane gl holds rows gl*RX .. gl*RX+RX-1)
+template <int NX, int RX, int W, class X, int S = 0>
+BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[NX]) {
+  if constexpr (S < W) {
+#pragma unroll
+    for (int r = 0; r < RX; ++r)
+      if (S * RX + r < NX) full[S * RX + r] = ex.template tget<S>(mine[r]);
+    task_gather<NX, RX, W, X, S + 1>(ex, mine, full);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // KKT factorisation
 // ------------------------------------------------------------------------------------
@@ -1514,75 +1525,245 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
   }
   ex.sync();
   BMPC_TIC(t_ric);
-  // ---- tree Riccati factorisation (leaves -> root), one lane per branch --------------------
-  // The cost-to-go P runs backward along each branch in registers; only at a branch end are
-  // the children's first-node P read back (written by the previous depth phase).
+  // ---- tree Riccati factorisation (leaves -> root), one task group per branch ----------------
+  // A group of W = X::kTaskLanes lanes (a DPP quad) runs a branch; lane gl owns rows
+  // gl*RX .. of the node matrices, carries its rows of the cost-to-go P backward along the
+  // branch, and gathers the full A, B, M = Pb A, Pb B and P rows it needs from the group by DPP
+  // broadcasts -- every sum is the one riccati_step forms, term for term (bit-identical), but a
+  // lane holds a quarter of the node data (one lane per branch spilled the Riccati state to
+  // scratch on every node).  Only at a branch end are the children's first-node P rows read back.
   const gdouble* Ad = ws + L.Ad;
   const gdouble* Bd = ws + L.Bd;
+  constexpr int W = X::kTaskLanes;
+  constexpr int RX = (NX + W - 1) / W;
+  const int gl = ex.lane % W, grp = ex.lane / W, ngrp = ex.nlanes / W;
   double bad = 0.0;
+  // the full NX x NC matrix of row-distributed rows (lane gl: rows gl*RX + q)
+  auto gather_rows = [&](const auto& mine, auto& full) {
+    constexpr int NC = sizeof(full[0]) / sizeof(double);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      double col[RX], fc[NX];
+#pragma unroll
+      for (int q = 0; q < RX; ++q) col[q] = mine[q][c];
+      task_gather<NX, RX, W>(ex, col, fc);
+#pragma unroll
+      for (int r = 0; r < NX; ++r) full[r][c] = fc[r];
+    }
+  };
+  // Lane-varying picks (row gi's column of a matrix every lane holds) are taken while the
+  // values are formed, as selects between fresh values: a select chain over a register array's
+  // elements would be folded into a runtime index, i.e. the array moved to scratch memory.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
-    for (int bi = ex.lane; bi < nbd; bi += ex.nlanes) {
+    const int rounds = (nbd + ngrp - 1) / ngrp;
+    for (int rd = 0; rd < rounds; ++rd) {
+      const int bi = rd * ngrp + grp;
+      if (bi >= nbd) continue;   // whole group idle together
       const int b = b0 + bi;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
-      double Pn[NX][NX];
+      double Pn[RX][NX];   // this lane's rows of the cost-to-go after the current node
       if (leaf) {   // terminal node: P = hx
-        mat_load(Pn, ws + L.hx + (ndx + len) * NX * NX);
-        mat_store(Pn, ws + L.P + (ndx + len) * NX * NX);
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Pn[q][j] = ws[L.hx + (ndx + len) * NX * NX + i * NX + j];
+          if (gl * RX + q < NX)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) ws[L.P + (ndx + len) * NX * NX + i * NX + j] = Pn[q][j];
+        }
       }
-      for (int j = len - 1; j >= 0; --j) {
-        const int k = ndx + j, u = ndu + j;
-        // every operand of the node first (they do not depend on the recursion)
-        double Hx[NX][NX], Hu[NU][NU], A[NX][NX], B[NX][NU];
-        mat_load(Hx, ws + L.hx + k * NX * NX);
+      for (int jn = len - 1; jn >= 0; --jn) {
+        const int k = ndx + jn, u = ndu + jn;
+        // this lane's rows of the node's data (independent of the recursion)
+        double Hx[RX][NX], Ar[RX][NX], Ac[RX][NX], Br[RX][NU], Hu[NU][NU];
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Hx[q][j] = ws[L.hx + k * NX * NX + i * NX + j];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Ar[q][j] = Ad[u * NX * NX + i * NX + j];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) Ac[q][j] = Ad[u * NX * NX + j * NX + i];   // column i
+#pragma unroll
+          for (int m = 0; m < NU; ++m) Br[q][m] = Bd[u * NX * NU + i * NU + m];
+        }
         mat_load(Hu, ws + L.hu + u * NU * NU);
-        mat_load(A, Ad + u * NX * NX);
-        mat_load(B, Bd + u * NX * NU);
-        double Pb[NX][NX];
-        if (j < len - 1 || leaf) {
-          mat_copy(Pn, Pb);
+        double Pb[RX][NX];
+        if (jn < len - 1 || leaf) {
+#pragma unroll
+          for (int q = 0; q < RX; ++q)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Pb[q][c] = Pn[q][c];
         } else {
-          // the children's first-node P (written by the previous depth phase), loaded together
-          mat_zero(Pb);
+          // the children's first-node P rows (written by the previous depth phase), in the
+          // order riccati_step's caller sums them (pairs, the odd one padded with weight 0)
+#pragma unroll
+          for (int q = 0; q < RX; ++q)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Pb[q][c] = 0.0;
           const int c0 = t.br_child0[b];
           for (int i0 = 0; i0 < P.m; i0 += 2) {
-            double Pc[2][NX][NX];
+            double Pc[2][RX][NX];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              const int i = i0 + h < P.m ? i0 + h : i0;
-              mat_load(Pc[h], ws + L.P + t.br_ndx[c0 + i] * NX * NX);
+              const int ch = i0 + h < P.m ? i0 + h : i0;
+#pragma unroll
+              for (int q = 0; q < RX; ++q) {
+                const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+                for (int c = 0; c < NX; ++c) Pc[h][q][c] = ws[L.P + t.br_ndx[c0 + ch] * NX * NX + i * NX + c];
+              }
             }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const double w = i0 + h < P.m ? 1.0 : 0.0;
 #pragma unroll
-              for (int r = 0; r < NX; ++r)
+              for (int q = 0; q < RX; ++q)
 #pragma unroll
-                for (int c = 0; c < NX; ++c) Pb[r][c] += w * Pc[h][r][c];
+                for (int c = 0; c < NX; ++c) Pb[q][c] += w * Pc[h][q][c];
             }
           }
         }
-        if (!riccati_step<NX, NU>(Hx, Hu, A, B, Pb, Pn, ws + L.Luu + u * NU * NU, ws + L.Kg + u * NU * NX))
-          bad = 1.0;
-        mat_store(Pn, ws + L.P + k * NX * NX);
+        // full A and B (every lane)
+        double Af[NX][NX], Bf[NX][NU];
+        gather_rows(Ar, Af);
+        gather_rows(Br, Bf);
+        // M = Pb A (own rows), then the full M
+        double Mr[RX][NX], Mf[NX][NX];
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Pb[q][r] * Af[r][j];
+            Mr[q][j] = v;
+          }
+        gather_rows(Mr, Mf);
+        // Pk = Hx + A'M (own rows)
+        double Pk[RX][NX];
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Ac[q][r] * Mf[r][j];
+            Pk[q][j] = Hx[q][j] + v;
+          }
+        // Qux = B'M and Quu = Hu + B'(Pb B) (full, every lane)
+        double Qux[NU][NX], Quu[NU][NU], qc[RX][NU];   // qc: column gl*RX+q of Qux
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Bf[r][i] * Mf[r][j];
+            Qux[i][j] = v;
+#pragma unroll
+            for (int q = 0; q < RX; ++q) qc[q][i] = (j == gl * RX + q || j == 0) ? v : qc[q][i];
+          }
+        double PBr[RX][NU], PBf[NX][NU];   // Pb B
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+#pragma unroll
+          for (int j = 0; j < NU; ++j) {
+            double pb = 0.0;
+#pragma unroll
+            for (int c = 0; c < NX; ++c) pb += Pb[q][c] * Bf[c][j];
+            PBr[q][j] = pb;
+          }
+        gather_rows(PBr, PBf);
+        mat_copy(Hu, Quu);
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+          for (int j = 0; j < NU; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Bf[r][i] * PBf[r][j];
+            Quu[i][j] += v;
+          }
+        if (!chol<NU>(Quu)) bad = 1.0;
+        double Qi[NU][NU];   // Quu^-1 (the tree sweeps multiply by it)
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+          double col[NU];
+#pragma unroll
+          for (int i = 0; i < NU; ++i) col[i] = i == j ? 1.0 : 0.0;
+          chol_solve<NU>(Quu, col);
+#pragma unroll
+          for (int i = 0; i < NU; ++i) Qi[i][j] = col[i];
+        }
+        double K[NU][NX], kc[RX][NU];   // kc: column gl*RX+q of K
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          double col[NU];
+#pragma unroll
+          for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
+          chol_solve<NU>(Quu, col);
+#pragma unroll
+          for (int i = 0; i < NU; ++i) {
+            K[i][j] = col[i];
+#pragma unroll
+            for (int q = 0; q < RX; ++q) kc[q][i] = (j == gl * RX + q || j == 0) ? col[i] : kc[q][i];
+          }
+        }
+        // Pk += Qux' K (own rows), then symmetrise: P[i][j] = P[j][i] = (P[lo][hi] + P[hi][lo]) / 2
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NU; ++r) v += qc[q][r] * K[r][j];
+            Pk[q][j] += v;
+          }
+        // column gl*RX+q of the full Pk, gathered column by column
+        double pcol[RX][NX];
+#pragma unroll
+        for (int c = 0; c < NX; ++c) {
+          double cm[RX], fc[NX];
+#pragma unroll
+          for (int q = 0; q < RX; ++q) cm[q] = Pk[q][c];
+          task_gather<NX, RX, W>(ex, cm, fc);
+#pragma unroll
+          for (int q = 0; q < RX; ++q)
+#pragma unroll
+            for (int r = 0; r < NX; ++r) pcol[q][r] = (c == gl * RX + q || c == 0) ? fc[r] : pcol[q][r];
+        }
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            const double pij = Pk[q][j], pji = pcol[q][j];   // own row entry, column entry
+            Pn[q][j] = i == j ? pij : i < j ? 0.5 * (pij + pji) : 0.5 * (pji + pij);
+          }
+        }
+        // stores: P rows, K columns (lane gl: entries j = gl*RX + q), Quu^-1 (lane gl 0)
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q;
+          if (i < NX) {
+#pragma unroll
+            for (int j = 0; j < NX; ++j) ws[L.P + k * NX * NX + i * NX + j] = Pn[q][j];
+#pragma unroll
+            for (int m = 0; m < NU; ++m) ws[L.Kg + u * NU * NX + m * NX + i] = kc[q][m];
+          }
+        }
+        if (gl == 0) mat_store(Qi, ws + L.Luu + u * NU * NU);
       }
     }
     ex.sync();
   }
   BMPC_TOC(C.ws, L, 23, t_ric);
   return ex.max(bad) == 0.0;
-}
-
-// all NX entries of a row-distributed vector (lane gl holds rows gl*RX .. gl*RX+RX-1)
-template <int NX, int RX, int W, class X, int S = 0>
-BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[NX]) {
-  if constexpr (S < W) {
-#pragma unroll
-    for (int r = 0; r < RX; ++r)
-      if (S * RX + r < NX) full[S * RX + r] = ex.template tget<S>(mine[r]);
-    task_gather<NX, RX, W, X, S + 1>(ex, mine, full);
-  }
 }
 
 // one backward Riccati-sweep node of a task: g (successor terms, own rows) -> l, kf
