@@ -65,11 +65,12 @@ struct BandQPWs {
 };
 
 BMPC_HD size_t bandqp_stride(int nk, int W) { return 2 * (size_t)nk * W + 11 * (size_t)nk; }
-// LDS: the factorisation window (W*W), its column of multipliers (W), the solve vector (nk),
-// then (lb_lds) the factor itself (nk*W): the eight triangular sweeps of an iteration then
-// read LDS instead of global memory
+// LDS: the column of multipliers (W) and the solve vector (nk), then either the factorisation
+// window (W*W; the factor goes to the workspace) or (lb_lds) the whole band, factored in
+// place (nk*W): no row streamed from global memory inside the column loop, and the
+// triangular sweeps of an iteration read LDS
 BMPC_HD size_t bandqp_lds_doubles(int nk, int W, bool lb_lds) {
-  return (size_t)W * W + W + nk + (lb_lds ? (size_t)nk * W : 0);
+  return (size_t)W + nk + (lb_lds ? (size_t)nk * W : (size_t)W * W);
 }
 
 BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
@@ -103,15 +104,43 @@ BMPC_HD void bqp_matvec(const X& ex, const BandQPDesc& d, const double* Kb, cons
   ex.sync();
 }
 
+// Rank-1 update pattern of one column: entry (a, b), 0 <= b <= a < last, of the active
+// rows' lower triangle, flattened t = a(a+1)/2 + b and dealt round-robin over the lanes (a
+// lane per row would leave lane a with a+1 dependent updates, the others idle)
+template <class X, class F>
+BMPC_HD void bqp_tri_for(const X& ex, int last, F f) {
+  const int ntri = last * (last + 1) / 2;
+  int a = 0, b = ex.lane;
+  while (b > a) {
+    b -= a + 1;
+    ++a;
+  }
+  for (int t = ex.lane; t < ntri; t += ex.nlanes) {
+    f(a, b);
+    b += ex.nlanes;
+    while (b > a) {
+      b -= a + 1;
+      ++a;
+    }
+  }
+}
+
+// the pivot of column k: a pivot of the wrong sign or below 1e-13 in magnitude is replaced
+// by +-2e-7 (ECOS's dynamic regularisation constants)
+BMPC_HD double bqp_pivot(const BandQPDesc& d, int k, double dk) {
+  const double sg = d.kind[k] == QPK_X ? 1.0 : -1.0;
+  return sg * dk >= 1e-13 ? dk : sg * 2e-7;
+}
+
 // Band LDL' of Kb with diagonal fdg (the regularised one) into Lb: row i of Lb holds
 // L[i][i-k] for k = 1..bw and D[i] at k = 0.  Right-looking, rows k..k+bw of the active
-// submatrix resident in the LDS ring window.  A pivot of the wrong sign or below 1e-13 in
-// magnitude is replaced by +-2e-7 (ECOS's dynamic regularisation constants).
+// submatrix resident in the LDS ring window; the row that enters the window after column k
+// is loaded before the column's arithmetic (its latency hides behind it).
 template <class X, class LP>
 BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* Lb) {
   const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
-  auto* win = ex.lds;
-  auto* lv = ex.lds + (size_t)W * W;
+  auto* lv = ex.lds;
+  auto* win = ex.lds + W + nk;
   const int rows0 = nk < W ? nk : W;
   for (int t = ex.lane; t < rows0 * W; t += nl) {
     const int i = t / W, k = t - i * W;
@@ -119,31 +148,52 @@ BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, cons
   }
   ex.sync();
   for (int k = 0; k < nk; ++k) {
-    const int slot = k % W;
-    double dk = win[slot * W];
-    const double sg = d.kind[k] == QPK_X ? 1.0 : -1.0;
-    if (!(sg * dk >= 1e-13)) dk = sg * 2e-7;
+    const int slot = k % W, nxt = k + W;
+    double pre = 0.0;   // this lane's entry c = lane of row nxt (W <= nlanes; else loaded at retirement)
+    if (nxt < nk && ex.lane < W) pre = ex.lane == 0 ? fdg[nxt] : Kb[(size_t)nxt * W + ex.lane];
+    const double dk = bqp_pivot(d, k, win[slot * W]);
     const int last = nk - 1 - k < bw ? nk - 1 - k : bw;   // rows k+1 .. k+last
     for (int a = ex.lane; a < last; a += nl) {
-      const int i = k + 1 + a;
-      const int si = i % W;
+      const int si = (k + 1 + a) % W;
       const double l = win[si * W + a + 1] / dk;
       win[si * W + a + 1] = l;
       lv[a] = l;
     }
     ex.sync();
-    for (int a = ex.lane; a < last; a += nl) {
-      const int si = (k + 1 + a) % W;
-      const double la = lv[a] * dk;
-      for (int b = 0; b <= a; ++b) win[si * W + a - b] -= la * lv[b];
-    }
+    bqp_tri_for(ex, last, [&](int a, int b) { win[((k + 1 + a) % W) * W + a - b] -= lv[a] * dk * lv[b]; });
     ex.sync();
-    // row k is final: retire it to Lb and stream row k + W into its slot
-    const int nxt = k + W;
+    // row k is final: retire it to Lb and put row k + W into its slot
     for (int c = ex.lane; c < W; c += nl) {
       Lb[(size_t)k * W + c] = c == 0 ? dk : win[slot * W + c];
-      if (nxt < nk) win[slot * W + c] = c == 0 ? fdg[nxt] : Kb[(size_t)nxt * W + c];
+      if (nxt < nk) win[slot * W + c] = c < nl ? pre : (c == 0 ? fdg[nxt] : Kb[(size_t)nxt * W + c]);
     }
+    ex.sync();
+  }
+}
+
+// The same factorisation with the whole band in LDS (lb_lds), factored in place: one copy
+// in, then per column the multipliers and the rank-1 update, all LDS.
+template <class X, class LP>
+BMPC_HD void bqp_factor_lds(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* L) {
+  const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
+  auto* lv = ex.lds;
+  for (size_t t = ex.lane; t < (size_t)nk * W; t += nl) {
+    const size_t i = t / W;
+    L[t] = t == i * W ? fdg[i] : Kb[t];
+  }
+  ex.sync();
+  for (int k = 0; k < nk; ++k) {
+    const double dk = bqp_pivot(d, k, L[(size_t)k * W]);
+    const int last = nk - 1 - k < bw ? nk - 1 - k : bw;
+    for (int a = ex.lane; a < last; a += nl) {
+      LP* e = L + (size_t)(k + 1 + a) * W + a + 1;
+      const double l = *e / dk;
+      *e = l;
+      lv[a] = l;
+    }
+    if (ex.lane == 0) L[(size_t)k * W] = dk;
+    ex.sync();
+    bqp_tri_for(ex, last, [&](int a, int b) { L[(size_t)(k + 1 + a) * W + a - b] -= lv[a] * dk * lv[b]; });
     ex.sync();
   }
 }
@@ -152,7 +202,7 @@ BMPC_HD void bqp_factor(const X& ex, const BandQPDesc& d, const double* Kb, cons
 template <class X, class LP>
 BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const LP* Lb, const double* b, double* out) {
   const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
-  auto* y = ex.lds + (size_t)W * W + W;
+  auto* y = ex.lds + W;
   for (int i = ex.lane; i < nk; i += nl) y[i] = b[i];
   ex.sync();
   for (int k = 0; k < nk; ++k) {            // L y = b
@@ -210,7 +260,13 @@ BMPC_HD double bqp_step(const X& ex, const BandQPDesc& d, const BandQPWs& v) {
   return ex.min(a);
 }
 
-template <class X, class LP>
+template <bool InLds, class X, class LP>
+BMPC_HD void bqp_factor_any(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* Lb) {
+  if constexpr (InLds) bqp_factor_lds(ex, d, Kb, fdg, Lb);
+  else bqp_factor(ex, d, Kb, fdg, Lb);
+}
+
+template <bool InLds, class X, class LP>
 BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
                            LP* Lb, double* x, double* y, int* iters) {
   const int nk = d.nk, nl = ex.nlanes, lane = ex.lane;
@@ -242,7 +298,7 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
     v.rhs[i] = kd == QPK_X ? -v.c[i] : v.c[i];
   }
   ex.sync();
-  bqp_factor(ex, d, v.Kb, v.fdg, Lb);
+  bqp_factor_any<InLds>(ex, d, v.Kb, v.fdg, Lb);
   bqp_solve_refined(ex, d, v, Lb, v.rhs, v.w);
   for (int i = lane; i < nk; i += nl) {
     v.t2[i] = d.kind[i] == QPK_X ? v.w[i] : 0.0;
@@ -315,7 +371,7 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
       v.rhs[i] = kd == QPK_IN ? -v.r[i] + v.s[i] : -v.r[i];
     }
     ex.sync();
-    bqp_factor(ex, d, v.Kb, v.fdg, Lb);
+    bqp_factor_any<InLds>(ex, d, v.Kb, v.fdg, Lb);
     // ---- predictor (affine) step
     bqp_solve_refined(ex, d, v, Lb, v.rhs, v.dw);
     for (int i = lane; i < nk; i += nl)
@@ -367,8 +423,8 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
 template <class X>
 BMPC_HD int bandqp_solve(const X& ex, const BandQPDesc& d, const double* vals, const double* cvals, double* ws,
                          double* x, double* y, int* iters) {
-  if (d.lb_lds) return bandqp_solve_t(ex, d, vals, cvals, ws, ex.lds + (size_t)d.W * d.W + d.W + d.nk, x, y, iters);
-  return bandqp_solve_t(ex, d, vals, cvals, ws, bandqp_ws(d, ws).Lb, x, y, iters);
+  if (d.lb_lds) return bandqp_solve_t<true>(ex, d, vals, cvals, ws, ex.lds + d.W + d.nk, x, y, iters);
+  return bandqp_solve_t<false>(ex, d, vals, cvals, ws, bandqp_ws(d, ws).Lb, x, y, iters);
 }
 
 }  // namespace bmpc

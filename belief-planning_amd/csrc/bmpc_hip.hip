@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -160,10 +161,58 @@ hipError_t upload(DevBuf& b, const void* host, size_t bytes) {
 
 }  // namespace
 
+namespace {
+// A grow-only device buffer (reallocated only when a call needs more).
+struct GrowBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  GrowBuf() = default;
+  GrowBuf(const GrowBuf&) = delete;
+  GrowBuf& operator=(const GrowBuf&) = delete;
+  ~GrowBuf() {
+    if (p) hipFree(p);
+  }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// bmpc_qp_solve's analyses, keyed by everything bandqp_analyse reads except the bound
+// values: the pattern, the row classes, max_iter, eps and the factor-in-LDS choice.  A caller
+// such as PredictiveControllers.MPC or Highway_env re-solves one pattern every control step:
+// the ordering, the scatter lists and their device copy are made once.
+struct QPCacheEntry {
+  std::vector<int32_t> key;
+  double eps = 0;
+  HostBandQP h;
+  GrowBuf tab;
+  uint64_t used = 0;
+};
+}  // namespace
+
 struct bmpc_ctx {
   int device;
   int cus;             // compute units (hipDeviceProp_t::multiProcessorCount)
   size_t lds_per_cu;   // LDS bytes per CU (maxSharedMemoryPerMultiProcessor)
+  // bmpc_qp_solve: its own stream (synchronised alone, never the device), the analysis cache
+  // and grow-only buffers reused across calls
+  hipStream_t qstream = nullptr;
+  static constexpr int kQPCache = 8;
+  std::vector<std::unique_ptr<QPCacheEntry>> qcache;
+  uint64_t qclock = 0;
+  GrowBuf q_in, q_ws, q_out;
+  std::vector<double> q_host;
+  ~bmpc_ctx() {
+    if (qstream) hipStreamDestroy(qstream);
+  }
 };
 
 struct bmpc_plan {
@@ -212,7 +261,11 @@ int bmpc_open(int hip_device, bmpc_ctx** out) {
   HIPCHECK(hipGetDeviceProperties(&prop, hip_device));
   const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   const size_t lds = prop.maxSharedMemoryPerMultiProcessor > 0 ? prop.maxSharedMemoryPerMultiProcessor : 160 * 1024;
-  *out = new bmpc_ctx{hip_device, cus, lds};
+  bmpc_ctx* c = new bmpc_ctx;
+  c->device = hip_device;
+  c->cus = cus;
+  c->lds_per_cu = lds;
+  *out = c;
   return 0;
 }
 
@@ -812,9 +865,44 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
                   const double* u, int max_iter, double eps, double* x, double* y, int32_t* status, int32_t* iters,
                   int32_t* info) {
   if (!ctx || !q || !x || !status) return fail(-22, "null argument");
-  HostBandQP h;
-  std::string err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, h, ctx->cus, ctx->lds_per_cu);
+  if (n < 1 || m < 0 || batch < 1 || !Pp || !Ap) return fail(-22, "need n >= 1, m >= 0, batch >= 1 and a pattern");
+  // the bounds of every problem are checked on every call; the analysis is looked up by
+  // pattern + row classes (bandqp_analyse validates the pattern on a miss)
+  std::vector<int> cls;
+  std::string err = bandqp_classify(m, batch, l, u, cls);
   if (!err.empty()) return fail(-22, err);
+  const bool lds_ok = batch <= ctx->cus;   // bandqp_analyse's factor-in-LDS rule depends on this only
+  std::vector<int32_t> key;
+  key.reserve(6 + 2 * (size_t)n + Pp[n] + Ap[n] + m);
+  key.insert(key.end(), {n, m, max_iter, lds_ok ? 1 : 0, Pp[n], Ap[n]});
+  key.insert(key.end(), Pp, Pp + n + 1);
+  key.insert(key.end(), Ap, Ap + n + 1);
+  if (Pp[n] > 0) key.insert(key.end(), Pi, Pi + Pp[n]);
+  if (Ap[n] > 0) key.insert(key.end(), Ai, Ai + Ap[n]);
+  key.insert(key.end(), cls.begin(), cls.end());
+  QPCacheEntry* ent = nullptr;
+  for (auto& c : ctx->qcache)
+    if (c->eps == eps && c->key == key) ent = c.get();
+  HIPCHECK(hipSetDevice(ctx->device));
+  if (!ent) {
+    auto fresh = std::make_unique<QPCacheEntry>();
+    err = bandqp_analyse(n, m, Pp, Pi, Ap, Ai, batch, l, u, max_iter, eps, fresh->h, ctx->cus, ctx->lds_per_cu);
+    if (!err.empty()) return fail(-22, err);
+    fresh->key.swap(key);
+    fresh->eps = eps;
+    HIPCHECK(fresh->tab.reserve(fresh->h.blob.size() * sizeof(int32_t)));
+    HIPCHECK(hipMemcpy(fresh->tab.p, fresh->h.blob.data(), fresh->h.blob.size() * sizeof(int32_t),
+                       hipMemcpyHostToDevice));
+    if ((int)ctx->qcache.size() >= bmpc_ctx::kQPCache) {   // evict the least recently used
+      auto lru = std::min_element(ctx->qcache.begin(), ctx->qcache.end(),
+                                  [](const auto& a, const auto& b) { return a->used < b->used; });
+      ctx->qcache.erase(lru);
+    }
+    ent = fresh.get();
+    ctx->qcache.push_back(std::move(fresh));
+  }
+  ent->used = ++ctx->qclock;
+  const HostBandQP& h = ent->h;
   const int nnzP = Pp[n], nnzA = Ap[n];
   if ((nnzP && !Px) || (nnzA && !Ax)) return fail(-22, "null value array");
   if (info) {
@@ -823,34 +911,35 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
     info[2] = h.d.n_in;
     info[3] = h.d.nscat;
   }
-  HIPCHECK(hipSetDevice(ctx->device));
+  if (!ctx->qstream) HIPCHECK(hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking));
+  hipStream_t st = ctx->qstream;
   const size_t B = (size_t)batch;
-  // host values in the kernel's per-problem order: [Px; Ax] and [q; l; u]
-  std::vector<double> vals(B * h.d.nvals), cvals(B * h.d.ncvals);
+  // host values in the kernel's per-problem order: [Px; Ax] then [q; l; u], one upload
+  const size_t nv = std::max<size_t>(B * h.d.nvals, 1), nc = B * h.d.ncvals;
+  std::vector<double>& hv = ctx->q_host;
+  hv.resize(nv + nc);
   for (size_t b = 0; b < B; ++b) {
-    double* v = vals.data() + b * h.d.nvals;
+    double* v = hv.data() + b * h.d.nvals;
     if (nnzP) memcpy(v, Px + b * nnzP, nnzP * sizeof(double));
     if (nnzA) memcpy(v + nnzP, Ax + b * nnzA, nnzA * sizeof(double));
-    double* c = cvals.data() + b * h.d.ncvals;
+    double* c = hv.data() + nv + b * h.d.ncvals;
     memcpy(c, q + b * n, n * sizeof(double));
     if (m) {
       memcpy(c + n, l + b * m, m * sizeof(double));
       memcpy(c + n + m, u + b * m, m * sizeof(double));
     }
   }
-  DevBuf dtab, dvals, dcvals, dws, dout;
-  HIPCHECK(upload(dtab, h.blob.data(), h.blob.size() * sizeof(int32_t)));
-  HIPCHECK(upload(dvals, vals.data(), std::max<size_t>(vals.size(), 1) * sizeof(double)));
-  HIPCHECK(upload(dcvals, cvals.data(), cvals.size() * sizeof(double)));
-  HIPCHECK(dws.alloc(B * h.d.stride * sizeof(double)));
+  HIPCHECK(ctx->q_in.reserve(hv.size() * sizeof(double)));
+  HIPCHECK(ctx->q_ws.reserve(B * h.d.stride * sizeof(double)));
   const size_t nout = B * (n + m) * sizeof(double) + 2 * B * sizeof(int32_t);
-  HIPCHECK(dout.alloc(nout));
-  double* dx = dout.as<double>();
+  HIPCHECK(ctx->q_out.reserve(nout));
+  HIPCHECK(hipMemcpyAsync(ctx->q_in.p, hv.data(), hv.size() * sizeof(double), hipMemcpyHostToDevice, st));
+  double* dx = ctx->q_out.as<double>();
   double* dy = dx + B * n;
   int32_t* dst = reinterpret_cast<int32_t*>(dy + B * m);
   int32_t* dit = dst + B;
   BandQPDesc d = h.d;
-  const int32_t* base = dtab.as<int32_t>();
+  const int32_t* base = ent->tab.as<int32_t>();
   d.kind = base;
   d.scat = d.kind + h.kind.size();
   d.cscat = d.scat + h.scat.size();
@@ -858,14 +947,17 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
   d.ymap = d.xmap + h.xmap.size();
   const size_t lds = bandqp_lds_doubles(d.nk, d.W, d.lb_lds) * sizeof(double);
   if (lds > 64 * 1024) HIPCHECK(hipFuncSetAttribute((const void*)k_bandqp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_bandqp, dim3(batch), dim3(64), lds, 0, d, dvals.as<double>(), dcvals.as<double>(),
-                     dws.as<double>(), dx, dy, dst, dit, batch);
+  hipLaunchKernelGGL(k_bandqp, dim3(batch), dim3(64), lds, st, d, ctx->q_in.as<double>(), ctx->q_in.as<double>() + nv,
+                     ctx->q_ws.as<double>(), dx, dy, dst, dit, batch);
   HIPCHECK(hipGetLastError());
-  HIPCHECK(hipDeviceSynchronize());
-  HIPCHECK(hipMemcpy(x, dx, B * n * sizeof(double), hipMemcpyDeviceToHost));
-  if (y && m) HIPCHECK(hipMemcpy(y, dy, B * m * sizeof(double), hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(status, dst, B * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (iters) HIPCHECK(hipMemcpy(iters, dit, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+  // one read-back of x | y | status | iters
+  std::vector<char> ho(nout);
+  HIPCHECK(hipMemcpyAsync(ho.data(), dx, nout, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  memcpy(x, ho.data(), B * n * sizeof(double));
+  if (y && m) memcpy(y, ho.data() + B * n * sizeof(double), B * m * sizeof(double));
+  memcpy(status, ho.data() + B * (n + m) * sizeof(double), B * sizeof(int32_t));
+  if (iters) memcpy(iters, ho.data() + B * (n + m) * sizeof(double) + B * sizeof(int32_t), B * sizeof(int32_t));
   return 0;
 }
 

@@ -93,6 +93,24 @@ std::vector<int> rcm(const std::vector<std::vector<int>>& adj) {
 
 }  // namespace
 
+std::string bandqp_classify(int m, int batch, const double* l, const double* u, std::vector<int>& cls) {
+  cls.assign(m > 0 ? m : 0, 0);
+  if (m > 0 && (!l || !u)) return "null pattern or bounds";
+  for (int b = 0; b < batch; ++b) {
+    const double* lb = l + (size_t)b * m;
+    const double* ub = u + (size_t)b * m;
+    for (int r = 0; r < m; ++r) {
+      const double lo = lb[r], hi = ub[r];
+      if (std::isnan(lo) || std::isnan(hi)) return fmt("NaN bound in row %ld (problem %ld)", r, b);
+      if (lo > hi) return fmt("l > u in row %ld (problem %ld)", r, b);
+      const int c = classify(lo, hi);
+      if (b == 0) cls[r] = c;
+      else if (c != cls[r]) return fmt("row %ld is classified differently in problem %ld (eq / one-sided / free)", r, b);
+    }
+  }
+  return "";
+}
+
 void HostBandQP::point_tables(const int32_t* base) {
   const int32_t* p = base;
   d.kind = p;
@@ -126,17 +144,9 @@ std::string bandqp_analyse(int n, int m, const int32_t* Pp, const int32_t* Pi, c
   }
   const int nnzP = Pp[n], nnzA = Ap[n];
   // ---- rows: one class for the whole batch
-  std::vector<int> cls(m);
-  for (int r = 0; r < m; ++r) {
-    for (int b = 0; b < batch; ++b) {
-      const double lo = l[(size_t)b * m + r], hi = u[(size_t)b * m + r];
-      if (std::isnan(lo) || std::isnan(hi)) return fmt("NaN bound in row %ld (problem %ld)", r, b);
-      if (lo > hi) return fmt("l > u in row %ld (problem %ld)", r, b);
-      const int c = classify(lo, hi);
-      if (b == 0) cls[r] = c;
-      else if (c != cls[r]) return fmt("row %ld is classified differently in problem %ld (eq / one-sided / free)", r, b);
-    }
-  }
+  std::vector<int> cls;
+  std::string err = bandqp_classify(m, batch, l, u, cls);
+  if (!err.empty()) return err;
   // ---- KKT indices before ordering: x, then per row its eq or upper / lower copies
   std::vector<int> k_up(m, -1), k_lo(m, -1), kindv(n, QPK_X);
   int nk = n, n_in = 0;

@@ -21,6 +21,10 @@ struct HostBandQP {
 // |v| >= this is an infinite bound (OSQP_INFTY is 1e30)
 constexpr double kQPInfinity = 1e20;
 
+// Check the bounds of every problem (no NaN, l <= u) and classify each row (equality /
+// one-sided / two-sided / free), alike across the batch.  Returns "" on success.
+std::string bandqp_classify(int m, int batch, const double* l, const double* u, std::vector<int>& cls);
+
 // Validate the CSC pattern (P upper triangular, n+1 column pointers; A m x n) and the bounds
 // of every problem (they must classify every row alike), then build everything.  Returns
 // "" on success, else an error message.
