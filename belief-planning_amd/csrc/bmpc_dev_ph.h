@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
 // an iteration makes at most seven -- RES, FAC+CPL+BKP, AFF+CMB, UPD and the refinement rounds
 // that run -- each with every operator inlined into it.
 template <class X, int NX, int NU, int G>
-__device__ __attribute__((noinline)) bool ph_group(const X ex, const Ctx Cin, int it) {
+__device__ __forceinline__ bool ph_group_body(const X ex, const Ctx Cin, int it) {
   // arguments arrive in VGPRs: the plan / layout / slab pointers back to SGPRs (scalar loads of
   // every Plan field instead of vector loads)
   const Ctx C = Cin.uniform();
@@ -130,7 +130,20 @@ __device__ __attribute__((noinline)) bool ph_group(const X ex, const Ctx Cin, in
   return true;
 }
 
-template <class M>
+// mode 2 calls each group out of line; mode 3 (INL) inlines every group into the kernel -- each
+// appears at one call site, so the kernel makes no device call at all (no callee-saved-register
+// round trips through scratch; only the register allocator's own spills remain)
+template <class X, int NX, int NU, int G>
+__device__ __attribute__((noinline)) bool ph_group_call(const X ex, const Ctx Cin, int it) {
+  return ph_group_body<X, NX, NU, G>(ex, Cin, it);
+}
+template <class X, int NX, int NU, int G, bool INL>
+__device__ __forceinline__ bool ph_group(const X ex, const Ctx Cin, int it) {
+  if constexpr (INL) return ph_group_body<X, NX, NU, G>(ex, Cin, it);
+  else return ph_group_call<X, NX, NU, G>(ex, Cin, it);
+}
+
+template <class M, bool INL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm_g(const PhArgs a) {
   if ((int)blockIdx.x >= a.batch) return;
   const int e = a.e0 + blockIdx.x;
@@ -148,20 +161,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   C.L = (CLayout*)&L;
   C.ws = (gdouble*)ws;
   const gdouble* st = C.ws + L.ist;
-  ph_group<X, NX, NU, 0>(ex, C, 0);
+  ph_group<X, NX, NU, 0, INL>(ex, C, 0);
   const int maxit = P.desc.maxit;
   if (ph_flag(ex, st, IS_ACTIVE))
     for (int it = 0; it <= maxit; ++it) {
-      ph_group<X, NX, NU, 1>(ex, C, it);
+      ph_group<X, NX, NU, 1, INL>(ex, C, it);
       if (it == maxit || !ph_flag(ex, st, IS_ACTIVE)) break;
-      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 2>(ex, C, it);
+      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 2, INL>(ex, C, it);
       const int nref = __builtin_amdgcn_readfirstlane((int)st[IS_NREF]);
       for (int r = 0; r < nref; ++r)
-        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 3>(ex, C, r);
-      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 4>(ex, C, it);
+        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 3, INL>(ex, C, r);
+      if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 4, INL>(ex, C, it);
       for (int r = 0; r < nref; ++r)
-        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 5>(ex, C, r);
-      if (!__builtin_amdgcn_readfirstlane((int)ph_group<X, NX, NU, 6>(ex, C, it))) break;
+        if (ph_flag(ex, st, IS_OK)) ph_group<X, NX, NU, 5, INL>(ex, C, r);
+      if (!__builtin_amdgcn_readfirstlane((int)ph_group<X, NX, NU, 6, INL>(ex, C, it))) break;
     }
   const IpmResult r = ph_result(st);
   ipm_unpack<X, M>(ex, P, L, ws, r);
@@ -197,13 +210,14 @@ hipError_t launch_ph(const SolveLaunch& s, const PhArgs& a, int it, hipStream_t 
 template <class M>
 hipError_t launch_ipm_phased(const SolveLaunch& s) {
   hipError_t e;
-  if (s.ph_mode == 2) {   // one kernel, grouped out-of-line phases
+  if (s.ph_mode == 2 || s.ph_mode == 3) {   // one kernel: grouped out-of-line phases / everything inlined
     const PhArgs a{s.bundle, s.ws, s.upred, s.xpred, s.bw, s.J, s.status, s.iters, s.d_count, 0, s.batch};
+    const void* kf = s.ph_mode == 3 ? (const void*)k_ipm_g<M, true> : (const void*)k_ipm_g<M, false>;
     if (s.lds_bytes > 64 * 1024 &&
-        (e = hipFuncSetAttribute((const void*)k_ipm_g<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)s.lds_bytes)) != hipSuccess)
+        (e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds_bytes)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(k_ipm_g<M>, dim3(a.batch), dim3(64), s.lds_bytes, s.stream, a);
+    if (s.ph_mode == 3) hipLaunchKernelGGL((k_ipm_g<M, true>), dim3(a.batch), dim3(64), s.lds_bytes, s.stream, a);
+    else hipLaunchKernelGGL((k_ipm_g<M, false>), dim3(a.batch), dim3(64), s.lds_bytes, s.stream, a);
     return hipGetLastError();
   }
   const int ns = s.nsub < 1 ? 1 : s.nsub > kMaxSub ? kMaxSub : s.nsub;
