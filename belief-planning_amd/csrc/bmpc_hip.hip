@@ -208,7 +208,7 @@ struct bmpc_ctx {
   static constexpr int kQPCache = 8;
   std::vector<std::unique_ptr<QPCacheEntry>> qcache;
   uint64_t qclock = 0;
-  GrowBuf q_in, q_ws, q_out;
+  GrowBuf q_in, q_ws, q_out, q_aux;
   std::vector<double> q_host;
   ~bmpc_ctx() {
     if (qstream) hipStreamDestroy(qstream);
@@ -833,30 +833,47 @@ int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const do
   const double* in_h[] = {hc, xb, u, xbackup};
   const size_t out_sz[] = {nb, nb * nb, nb * 2, nb, (size_t)M * m, (size_t)M * m * nb};
   double* out_h[] = {xbp, A, Bm, C, h0, Jh};
-  size_t tot = 0;
-  for (size_t v : in_sz) tot += v;
-  for (size_t v : out_sz) tot += (size_t)B * v;
-  DevBuf bbuf;
-  HIPCHECK(bbuf.alloc(tot * sizeof(double)));
-  double* buf = bbuf.as<double>();
-  double* cur = buf;
+  // one upload of the packed inputs, one read-back of the packed outputs, on the context's
+  // stream into its grow-only buffer (the belief MPC calls this once per control step)
+  size_t tin = 0, tout = 0;
+  for (size_t v : in_sz) tin += v;
+  for (int i = 0; i < 6; ++i) tout += out_h[i] ? (size_t)B * out_sz[i] : 0;
+  std::vector<double>& hv = ctx->q_host;
+  hv.resize(tin + tout);
+  {
+    double* c = hv.data();
+    for (int i = 0; i < 4; ++i) {
+      memcpy(c, in_h[i], in_sz[i] * sizeof(double));
+      c += in_sz[i];
+    }
+  }
+  HIPCHECK(ctx->q_aux.reserve((tin + tout) * sizeof(double)));
+  if (!ctx->qstream) HIPCHECK(hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking));
+  hipStream_t st = ctx->qstream;
+  double* buf = ctx->q_aux.as<double>();
+  HIPCHECK(hipMemcpyAsync(buf, hv.data(), tin * sizeof(double), hipMemcpyHostToDevice, st));
   double* din[4];
+  double* cur = buf;
   for (int i = 0; i < 4; ++i) {
     din[i] = cur;
-    HIPCHECK(hipMemcpy(cur, in_h[i], in_sz[i] * sizeof(double), hipMemcpyHostToDevice));
     cur += in_sz[i];
   }
   double* dout[6];
   for (int i = 0; i < 6; ++i) {
     dout[i] = out_h[i] ? cur : nullptr;
-    cur += (size_t)B * out_sz[i];
+    if (out_h[i]) cur += (size_t)B * out_sz[i];
   }
-  hipLaunchKernelGGL(k_hmm, dim3((B + 63) / 64), dim3(64), 0, 0, M, m, din[0], B, din[1], din[2], din[3], dout[0],
+  hipLaunchKernelGGL(k_hmm, dim3((B + 63) / 64), dim3(64), 0, st, M, m, din[0], B, din[1], din[2], din[3], dout[0],
                      dout[1], dout[2], dout[3], dout[4], dout[5]);
   HIPCHECK(hipGetLastError());
-  HIPCHECK(hipDeviceSynchronize());
+  if (tout) HIPCHECK(hipMemcpyAsync(hv.data() + tin, buf + tin, tout * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const double* o = hv.data() + tin;
   for (int i = 0; i < 6; ++i)
-    if (out_h[i]) HIPCHECK(hipMemcpy(out_h[i], dout[i], (size_t)B * out_sz[i] * sizeof(double), hipMemcpyDeviceToHost));
+    if (out_h[i]) {
+      memcpy(out_h[i], o, (size_t)B * out_sz[i] * sizeof(double));
+      o += (size_t)B * out_sz[i];
+    }
   return 0;
 }
 

@@ -49,10 +49,16 @@ def check_merge_replay(r, g, T):
     and the kernel's optima differ by up to ~1.2e-4 in the acceleration."""
     exits, J, u = (np.asarray(g[k][:T]) for k in ("traj_exit", "traj_J", "traj_u"))
     assert np.all(r["status"] >= 0), r["status"]
-    # exit 0 vs 10 at the rounding floor: the merge cost (~4e4) puts ECOS's 1e-8 gap at the
-    # precision floor of the structured KKT solve on ~1 step in 7 (host build 53 of 60 agree,
-    # GPU 50 of 60); the highway scenes hold 90%
-    assert np.mean(r["status"] == exits) >= 0.8, (r["status"], exits)
+    # exit 0 vs 10 at the rounding floor: the merge cost (~3e4) puts ECOS's 1e-8 relative gap at
+    # the precision floor of the structured KKT solve.  Traced on the host build's step 33 (it
+    # exits 10 where the recording exits 0): at iteration 20 pres 3.4e-10, dres 1.2e-10 but the
+    # relative gap is 1.55e-8 (> 1e-8); the next step meets the gap (2.3e-10) and lifts pres to
+    # 2.4e-8 (> 1e-8), the one after to 4.8e-5, the step then fails and ECOS backtracks to the
+    # best iterate (exit 10) -- the KKT solves refine to ~1e-15 of their scale throughout.  Host
+    # build 54 of 60 agree; the highway scenes hold 90%
+    agree = float(np.mean(r["status"] == exits))
+    print(f"merge replay: exit codes agree on {agree:.3f} of {T} steps")
+    assert agree >= 0.8, (r["status"], exits)
     for t in range(T):
         tight = exits[t] == 0 and r["status"][t] == 0
         rtol, atol = (1e-6, 5e-4) if tight else (1e-4, 5e-3)
