@@ -31,11 +31,29 @@
 // tests/hostsim with the 1-lane host executor.
 #pragma once
 
+#include <type_traits>
+
 #include "bmpc_core.h"
 
 namespace bmpc {
 
+// -DBMPC_BQP_PROF (device builds, experiments): s_memtime cycles of the factorisation, the
+// triangular sweeps and the mat-vecs of problem 0, printed at the end of its solve
+#if defined(BMPC_BQP_PROF) && defined(__HIP_DEVICE_COMPILE__)
+__device__ unsigned long long g_bqp_prof[8];
+#define BQP_TIC(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define BQP_TOC(i, v) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_bqp_prof[i] += __builtin_amdgcn_s_memtime() - (v)
+#else
+#define BQP_TIC(v) ((void)0)
+#define BQP_TOC(i, v) ((void)0)
+#endif
+
 enum { QPK_X = 0, QPK_EQ = 1, QPK_IN = 2 };
+
+#ifndef BMPC_BQP_NB
+#define BMPC_BQP_NB 8   // columns per block of the one-wave blocked band factorisation
+#endif
 
 // problem statuses (OSQP's status_val codes where one exists)
 enum { QP_SOLVED = 1, QP_MAX_ITER = -2, QP_NUMERICS = -8 };
@@ -69,8 +87,9 @@ BMPC_HD size_t bandqp_stride(int nk, int W) { return 2 * (size_t)nk * W + 11 * (
 // window (W*W; the factor goes to the workspace) or (lb_lds) the whole band, factored in
 // place (nk*W): no row streamed from global memory inside the column loop, and the
 // triangular sweeps of an iteration read LDS
+// (lb_lds adds the row signs (nk) and the blocked factorisation's panel copies, 2 * 64 * NB)
 BMPC_HD size_t bandqp_lds_doubles(int nk, int W, bool lb_lds) {
-  return (size_t)W + nk + (lb_lds ? (size_t)nk * W : (size_t)W * W);
+  return (size_t)W + nk + (lb_lds ? (size_t)nk * W + nk + 2 * 64 * BMPC_BQP_NB : (size_t)W * W);
 }
 
 BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
@@ -87,21 +106,46 @@ BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
   return v;
 }
 
-// out = K v, K the symmetric band matrix Kb with its diagonal replaced by dg
+// out = K v, K the symmetric band matrix Kb with its diagonal replaced by dg.  A lane's row
+// loads are issued in chunks of 8 (band entry and vector entry, indices clamped and the extra
+// terms masked by a zero factor), so a row costs bw / 4 memory round trips instead of 2 bw;
+// the terms are added in the same order as a plain row loop (lower part, then upper part).
 template <class X>
 BMPC_HD void bqp_matvec(const X& ex, const BandQPDesc& d, const double* Kb, const double* dg, const double* v,
                         double* out) {
   const int nk = d.nk, W = d.W, bw = d.bw;
+  constexpr int CH = 8;
+  BQP_TIC(t0);
   for (int i = ex.lane; i < nk; i += ex.nlanes) {
     double a = dg[i] * v[i];
-    const double* row = Kb + (size_t)i * W;
     const int k0 = i < bw ? i : bw;
-    for (int k = 1; k <= k0; ++k) a += row[k] * v[i - k];
     const int k1 = nk - 1 - i < bw ? nk - 1 - i : bw;
-    for (int k = 1; k <= k1; ++k) a += Kb[(size_t)(i + k) * W + k] * v[i + k];
+    for (int kb = 1; kb <= k0; kb += CH) {   // row i, columns i - k
+      double e[CH], x[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const bool in = kb + u <= k0;
+        e[u] = Kb[(size_t)i * W + (in ? kb + u : 0)];
+        x[u] = v[in ? i - kb - u : i];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) a += e[u] * (x[u] * (kb + u <= k0 ? 1.0 : 0.0));
+    }
+    for (int kb = 1; kb <= k1; kb += CH) {   // column i of the rows i + k below
+      double e[CH], x[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const bool in = kb + u <= k1;
+        e[u] = Kb[(size_t)(in ? i + kb + u : i) * W + (in ? kb + u : 0)];
+        x[u] = v[in ? i + kb + u : i];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) a += e[u] * (x[u] * (kb + u <= k1 ? 1.0 : 0.0));
+    }
     out[i] = a;
   }
   ex.sync();
+  BQP_TOC(2, t0);
 }
 
 // Rank-1 update pattern of one column: entry (a, b), 0 <= b <= a < last, of the active
@@ -226,9 +270,12 @@ BMPC_HD void bqp_ldl_solve(const X& ex, const BandQPDesc& d, const LP* Lb, const
 // out = K^{-1} b for the true matrix (Kb, diagonal tdg) through its regularised factor:
 // up to three refinement steps, stopping at a 1e-15 relative residual (oracle/qp_ipm.py).
 template <class X, class LP>
+BMPC_HD void bqp_ldl_solve_any(const X& ex, const BandQPDesc& d, const LP* Lb, const double* b, double* out);
+
+template <class X, class LP>
 BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs& v, const LP* Lb, const double* b,
                                double* out) {
-  bqp_ldl_solve(ex, d, Lb, b, out);
+  bqp_ldl_solve_any(ex, d, Lb, b, out);
   double bn = 0.0;
   for (int i = ex.lane; i < d.nk; i += ex.nlanes) bn = fmax(bn, fabs(b[i]));
   bn = ex.max(bn);
@@ -242,7 +289,7 @@ BMPC_HD void bqp_solve_refined(const X& ex, const BandQPDesc& d, const BandQPWs&
     rn = ex.max(rn);
     ex.sync();
     if (rn < 1e-15 * fmax(1.0, bn)) break;
-    bqp_ldl_solve(ex, d, Lb, v.t1, v.t2);
+    bqp_ldl_solve_any(ex, d, Lb, v.t1, v.t2);
     for (int i = ex.lane; i < d.nk; i += ex.nlanes) out[i] += v.t2[i];
     ex.sync();
   }
@@ -260,10 +307,190 @@ BMPC_HD double bqp_step(const X& ex, const BandQPDesc& d, const BandQPWs& v) {
   return ex.min(a);
 }
 
+// ---- one wave, band in LDS: blocked factorisation and sweeps ------------------------------
+// The column-at-a-time kernels above chain two barriers and an LDS round trip per column (and
+// per row of each sweep): one problem's solve is that chain, 20 ms for the belief MPC.  On a
+// single 64-lane wave (executors with kBqpWave) the band is processed in blocks of kBqpNB
+// columns: lane r holds row k0 + r of the block's kBqpNB + bw rows in registers, the block's
+// own column chain runs on wave broadcasts (readlane, no barrier), and the rest of the block's
+// work is one LDS pass.  Every entry receives the same updates in the same order as in the
+// column-at-a-time kernels (host build), so the factor and the solutions are the same numbers.
+constexpr int kBqpNB = BMPC_BQP_NB;
+template <class X, class = void>
+struct BqpWave : std::false_type {};
+template <class X>
+struct BqpWave<X, std::void_t<decltype(X::kBqpWave)>> : std::integral_constant<bool, X::kBqpWave> {};
+
+template <class X>
+BMPC_HD bool bqp_use_blk(const X&, const BandQPDesc& d) {
+  if constexpr (BqpWave<X>::value) return d.lb_lds && d.bw + kBqpNB <= 64;
+  else return false;
+}
+
+// LDS areas of the in-LDS layout: L (nk*W) after the multipliers (W) and the solve vector (nk),
+// then the row signs (nk), then the panel multipliers Pl and their pivot products Pw (64 x NB each)
+template <class X>
+BMPC_HD auto bqp_lds_sg(const X& ex, const BandQPDesc& d) { return ex.lds + d.W + d.nk + (size_t)d.nk * d.W; }
+
+template <class X, class LP>
+BMPC_HD void bqp_factor_blk(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* L) {
+  constexpr int NB = kBqpNB;
+  const int nk = d.nk, W = d.W, bw = d.bw, r = ex.lane;
+  const auto* sg = bqp_lds_sg(ex, d);
+  auto* Pl = bqp_lds_sg(ex, d) + nk;
+  auto* Pw = Pl + 64 * NB;
+  // the band in, loads batched 16 per lane (a load per loop trip would be a round trip each),
+  // then the regularised diagonal over it
+  lane_batch<16>(ex, 0, nk * W, [&](int t) { return Kb[t]; }, [&](int t, double v) { L[t] = v; });
+  ex.sync();
+  lane_batch<16>(ex, 0, nk, [&](int i) { return fdg[i]; }, [&](int i, double v) { L[(size_t)i * W] = v; });
+  ex.sync();
+  for (int k0 = 0; k0 < nk; k0 += NB) {
+    const int nb = nk - k0 < NB ? nk - k0 : NB;
+    const int nrow = nk - k0 < NB + bw ? nk - k0 : NB + bw;
+    const bool act = r < nrow;
+    const size_t rowW = (size_t)(act ? k0 + r : k0) * W;
+    // this lane's panel row: entry (k0 + r, k0 + j) at offset r - j (band and lower part only)
+    double a[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int off = r - j;
+      const bool in = act && j < nb && off >= 0 && off <= bw;
+      const double v = L[rowW + (in ? off : 0)];   // unconditional load, masked by arithmetic
+      a[j] = in ? v : 0.0;
+    }
+    const double sgr = act ? (double)sg[k0 + r] : 1.0;
+    BQP_TIC(tp);
+    double dj_[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (j < nb) {   // wave-uniform
+        double dj = ex.rlane(a[j], j);
+        const double sj = ex.rlane(sgr, j);
+        if (!(sj * dj >= 1e-13)) dj = sj * 2e-7;
+        dj_[j] = dj;
+        const double l = r > j ? a[j] / dj : 0.0;
+        a[j] = r > j ? l : (r == j ? dj : a[j]);
+        // rows above jj update an upper-triangle slot of column jj that is never read or
+        // written back, and columns past nb are never written back: no lane condition
+#pragma unroll
+        for (int jj = j + 1; jj < NB; ++jj) {
+          const double ljj = ex.rlane(l, jj);
+          a[jj] -= l * dj * ljj;
+        }
+      } else {
+        dj_[j] = 0.0;
+      }
+    }
+    // panel back to the band; rows past the block keep copies for the trailing update
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int off = r - j;
+      if (act && j < nb && off >= 0 && off <= bw) L[rowW + off] = a[j];
+      const bool below = act && r >= NB && j < nb && off <= bw;
+      Pl[j * 64 + r] = below ? a[j] : 0.0;   // column-major: lanes of consecutive rows hit consecutive banks
+      Pw[j * 64 + r] = below ? a[j] * dj_[j] : 0.0;
+    }
+    ex.sync();
+    BQP_TOC(4, tp);
+    BQP_TIC(tt);
+    // trailing update of rows / columns k0+NB .. k0+nrow-1 (all inside the band):
+    // entry (p, c) -= sum_j (l_pj d_j) l_cj, j in column order
+    bqp_tri_for(ex, nrow > NB ? nrow - NB : 0, [&](int pp, int cc) {
+      const int p = NB + pp, c = NB + cc;
+      LP* e = L + (size_t)(k0 + p) * W + (p - c);
+      double v = *e;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) v -= Pw[j * 64 + p] * Pl[j * 64 + c];
+      *e = v;
+    });
+    ex.sync();
+    BQP_TOC(5, tt);
+  }
+}
+
+// out = (L D L')^{-1} b with the factor in LDS: both sweeps in blocks of kBqpNB rows
+template <class X, class LP>
+BMPC_HD void bqp_ldl_solve_blk(const X& ex, const BandQPDesc& d, const LP* L, const double* b, double* out) {
+  constexpr int NB = kBqpNB;
+  const int nk = d.nk, W = d.W, bw = d.bw, r = ex.lane;
+  auto* y = ex.lds + W;
+  lane_batch<16>(ex, 0, nk, [&](int i) { return b[i]; }, [&](int i, double v) { y[i] = v; });
+  ex.sync();
+  BQP_TIC(tf);
+  for (int k0 = 0; k0 < nk; k0 += NB) {   // L y = b
+    const int nb = nk - k0 < NB ? nk - k0 : NB;
+    const int nrow = nk - k0 < NB + bw ? nk - k0 : NB + bw;
+    const bool act = r < nrow;
+    const int row = act ? k0 + r : k0;
+    double acc = y[row];
+    double lr[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int off = r - j;
+      const bool in = act && j < nb && off > 0 && off <= bw;
+      const double v = L[(size_t)row * W + (in ? off : 0)];
+      lr[j] = in ? v : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc -= lr[j] * ex.rlane(acc, j);   // lr = 0 off the band / above row j
+    if (act) y[row] = acc;
+    ex.sync();
+  }
+  BQP_TOC(6, tf);
+  for (int i = r; i < nk; i += 64) y[i] /= L[(size_t)i * W];
+  ex.sync();
+  BQP_TIC(tb);
+  for (int k1 = nk - 1; k1 > 0; k1 -= NB) {   // L' x = y, rows k1, k1 - 1, ... of the block
+    const int nb = k1 + 1 < NB ? k1 + 1 : NB;
+    const int nrow = k1 + 1 < NB + bw ? k1 + 1 : NB + bw;
+    const bool act = r < nrow;
+    const int row = act ? k1 - r : k1;
+    double acc = y[row];
+    double lr[NB];   // L[k1 - j][offset r - j]: the entry of row k1 - j in column k1 - r
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int off = r - j;
+      const bool in = act && j < nb && off > 0 && off <= bw;
+      const double v = L[(size_t)(in ? k1 - j : k1) * W + (in ? off : 0)];
+      lr[j] = in ? v : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc -= lr[j] * ex.rlane(acc, j);
+    if (act) y[row] = acc;
+    ex.sync();
+  }
+  BQP_TOC(7, tb);
+  lane_batch<16>(ex, 0, nk, [&](int i) { return (double)y[i]; }, [&](int i, double v) { out[i] = v; });
+  ex.sync();
+}
+
+template <class X, class LP>
+BMPC_HD void bqp_ldl_solve_any(const X& ex, const BandQPDesc& d, const LP* Lb, const double* b, double* out) {
+  BQP_TIC(t0);
+  if constexpr (BqpWave<X>::value) {
+    if (bqp_use_blk(ex, d)) bqp_ldl_solve_blk(ex, d, Lb, b, out);
+    else bqp_ldl_solve(ex, d, Lb, b, out);
+  } else {
+    bqp_ldl_solve(ex, d, Lb, b, out);
+  }
+  BQP_TOC(1, t0);
+}
+
 template <bool InLds, class X, class LP>
 BMPC_HD void bqp_factor_any(const X& ex, const BandQPDesc& d, const double* Kb, const double* fdg, LP* Lb) {
-  if constexpr (InLds) bqp_factor_lds(ex, d, Kb, fdg, Lb);
-  else bqp_factor(ex, d, Kb, fdg, Lb);
+  BQP_TIC(t0);
+  if constexpr (InLds) {
+    if constexpr (BqpWave<X>::value) {
+      if (bqp_use_blk(ex, d)) bqp_factor_blk(ex, d, Kb, fdg, Lb);
+      else bqp_factor_lds(ex, d, Kb, fdg, Lb);
+    } else {
+      bqp_factor_lds(ex, d, Kb, fdg, Lb);
+    }
+  } else {
+    bqp_factor(ex, d, Kb, fdg, Lb);
+  }
+  BQP_TOC(0, t0);
 }
 
 template <bool InLds, class X, class LP>
@@ -272,6 +499,11 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
   const int nk = d.nk, nl = ex.nlanes, lane = ex.lane;
   const BandQPWs v = bandqp_ws(d, ws);
   const double rs = 1e-8;   // static regularisation (ECOS's STATIC_REG)
+  BQP_TIC(t_all);
+  if (bqp_use_blk(ex, d)) {   // row signs of the pivot rule, for the blocked factorisation
+    auto* sg = bqp_lds_sg(ex, d);
+    for (int i = lane; i < nk; i += nl) sg[i] = d.kind[i] == QPK_X ? 1.0 : -1.0;
+  }
   // ---- assemble the band and the right-hand-side constants c (q | e | g by row kind)
   for (size_t t = lane; t < (size_t)nk * d.W; t += nl) v.Kb[t] = 0.0;
   for (int i = lane; i < nk; i += nl) v.c[i] = 0.0;
@@ -415,6 +647,15 @@ BMPC_HD int bandqp_solve_t(const X& ex, const BandQPDesc& d, const double* vals,
   }
   if (iters && lane == 0) *iters = it;
   ex.sync();
+  BQP_TOC(3, t_all);
+#if defined(BMPC_BQP_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    printf("bqp prof (cycles): factor %llu (panel %llu trailing %llu)  ldl_solve %llu (fwd %llu bwd %llu)  matvec %llu  "
+           "total %llu  iters %d\n", g_bqp_prof[0], g_bqp_prof[4], g_bqp_prof[5], g_bqp_prof[1], g_bqp_prof[6],
+           g_bqp_prof[7], g_bqp_prof[2], g_bqp_prof[3], it);
+    for (int i = 0; i < 8; ++i) g_bqp_prof[i] = 0;
+  }
+#endif
   return status;
 }
 

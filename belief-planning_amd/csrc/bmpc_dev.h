@@ -46,6 +46,13 @@ struct DevExecT {
   tab_ptr tab;   // topology tables (k_ipm / k_qp only)
   ldouble* eco;  // per-ego constants of the solve (ECO_*; kTransform only)
   static constexpr int nlanes = 64;
+  // one wave runs a band QP: blocked factorisation and sweeps on wave broadcasts (bmpc_bandqp.h)
+  static constexpr bool kBqpWave = true;
+  // lane l's v, wave-uniform (l uniform)
+  __device__ double rlane(double v, int l) const {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+  }
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
   // cone rows per lane the fused IPM passes hold in registers (bmpc_ipm.h, cone_regs)
