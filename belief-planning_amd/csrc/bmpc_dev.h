@@ -216,9 +216,14 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
   }
 }
 
-#ifndef BMPC_BLK_WAVES
-#define BMPC_BLK_WAVES 16   // waves per ego of the small-batch solver kernels (k_solve_blk)
+// waves per ego of the small-batch solver kernel (k_solve_blk): 4, or 8 for trees of at least
+// BMPC_BLK_WIDE_T state nodes (measured at one ego, profiles/r03/r03x_blk_waves.log: N=8 NB=2
+// 22 ms on 4 waves, 24 on 8, 38 on 16, 30 on one; N=20 NB=1 12-14 / 14-17 / 20-22 / 14-16;
+// N=30 NB=2 48-54 / 44-49 / 62-65 / 61-65)
+#ifndef BMPC_BLK_WIDE_T
+#define BMPC_BLK_WIDE_T 256
 #endif
+#define BMPC_BLK_WAVES_MAX 8
 
 // LDS of a multi-wave solver launch: the wave launch's, then the reduction scratch
 __host__ __device__ inline size_t solver_lds_bytes_blk(const Plan& P, bool transform, int nw) {
@@ -361,6 +366,7 @@ struct SolveLaunch {
   int32_t* h_count = nullptr;
   int maxit = 0;
   int ph_mode = 1;   // 1: one kernel per phase, 2: one kernel calling grouped out-of-line phases
+  int nw = 4;        // small-batch launch: waves per ego (4 or 8)
   int nsub = 1;                   // mode 1: sub-batches, one stream each
   hipStream_t* sub = nullptr;     // their streams [kMaxSub]
   hipEvent_t* sub_ev = nullptr;   // [kMaxSub + 1] fork / join events
@@ -395,9 +401,8 @@ hipError_t launch_solver(const SolveLaunch& a) {
 }
 
 // the small-batch launch: one ego per NW-wave workgroup (solver_lds_bytes_blk of LDS)
-template <class M, bool QP>
+template <class M, bool QP, int NW>
 hipError_t launch_blk_kernel(const SolveLaunch& a) {
-  constexpr int NW = BMPC_BLK_WAVES;
   if (a.lds_bytes > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_solve_blk<M, QP, NW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds_bytes);
@@ -407,12 +412,11 @@ hipError_t launch_blk_kernel(const SolveLaunch& a) {
                      a.pol, a.upred, a.xpred, a.bw, a.J, a.status, a.iters, a.batch);
   return hipGetLastError();
 }
+// (the OSQP-class controllers never take this path: bmpc_hip.hip chooses it for the CVaR IPM only)
 template <class M, bool WITH_QP>
 hipError_t launch_solver_blk(const SolveLaunch& a) {
-  if constexpr (WITH_QP) {
-    if (a.qp) return launch_blk_kernel<M, true>(a);
-  }
-  return launch_blk_kernel<M, false>(a);
+  if (a.qp) return hipErrorInvalidValue;
+  return a.nw == 8 ? launch_blk_kernel<M, false, 8>(a) : launch_blk_kernel<M, false, 4>(a);
 }
 
 // the per-model launchers (bmpc_k_highway.hip, bmpc_k_highway_t.hip, bmpc_k_merge.hip,

@@ -20,9 +20,6 @@ using namespace bmpc::dev;
 #ifndef BMPC_IPM_PHASED_DEFAULT
 #define BMPC_IPM_PHASED_DEFAULT 0
 #endif
-#ifndef BMPC_BLOCK_MIN_T
-#define BMPC_BLOCK_MIN_T 256   // state nodes of the smallest tree that takes the multi-wave small-batch path
-#endif
 #ifndef BMPC_PH_STREAMS_DEFAULT
 #define BMPC_PH_STREAMS_DEFAULT 4
 #endif
@@ -483,17 +480,18 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t, phased = launch_ipm_phased_highway_t;
   else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway, phased = launch_ipm_phased_highway;
   else if (merge) tree = launch_tree_merge, solver = launch_solver_merge, phased = launch_ipm_phased_merge;
-  // Small batches of large CVaR trees: one ego per 16-wave workgroup (k_solve_blk) when the
-  // batch leaves CUs idle.  Measured at one ego: N=30 NB=2 69-78 ms vs 105-109 ms on one wave;
-  // N=8 NB=2 41-47 vs 34-39 ms and N=20 NB=1 21-23 vs 15-17 ms (the extra barriers of the
-  // workgroup-wide reductions cost more than the wider loops save), hence the T threshold.
-  // BMPC_BLOCK_EGOS: the largest batch that takes this path (default: one ego per CU).
+  // Small batches of the CVaR IPM: one ego per multi-wave workgroup (k_solve_blk) when the batch
+  // leaves CUs idle -- 4 waves per ego, 8 for trees of BMPC_BLK_WIDE_T state nodes or more.
+  // Measured at one ego (profiles/r03/r03x_blk_waves.log): N=8 NB=2 22 ms vs 30 on one wave,
+  // N=20 NB=1 12-14 vs 14-16, N=30 NB=2 44-49 vs 61-65.  BMPC_BLOCK_EGOS: the largest batch that
+  // takes this path (default: one ego per CU; 0 disables it); BMPC_BLOCK_WAVES: 4 or 8.
   int blk_max = pl->ctx->cus;
   if (const char* e = getenv("BMPC_BLOCK_EGOS")) blk_max = atoi(e);
-  const bool blk = B <= blk_max && P.desc.controller == BMPC_CTRL_CVAR &&
-                   (P.T >= BMPC_BLOCK_MIN_T || getenv("BMPC_BLOCK_EGOS"));
+  const bool blk = B <= blk_max && P.desc.controller == BMPC_CTRL_CVAR;
   if (blk) {
-    a.lds_bytes = solver_lds_bytes_blk(P, xform, BMPC_BLK_WAVES);
+    a.nw = P.T >= BMPC_BLK_WIDE_T ? 8 : 4;
+    if (const char* e = getenv("BMPC_BLOCK_WAVES")) a.nw = atoi(e) == 8 ? 8 : 4;
+    a.lds_bytes = solver_lds_bytes_blk(P, xform, a.nw);
     a.rich = true;
     if (hwt) solver = launch_solver_blk_highway_t;
     else if (P.desc.model == BMPC_MODEL_HIGHWAY) solver = launch_solver_blk_highway;

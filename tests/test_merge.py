@@ -42,7 +42,7 @@ def replay_inputs(g, steps=None):
 
 
 def check_merge_replay(r, g, T):
-    """Exit codes agree on >= 80% of the steps.  Tolerances: J to 1e-6 relative (exit 0);
+    """Exit codes agree on >= 90% of the steps.  Tolerances: J to 1e-6 relative (exit 0);
     uPred[0] to 5e-4.  The merge cost is
     ~3e4, so ECOS's 1e-8 relative gap fixes J to ~3e-4 absolute, and through the input cost
     (R = diag(1, 100)) that only pins u to ~1e-2; late in the scene (u ~ 1e-2) the recorded
@@ -55,10 +55,11 @@ def check_merge_replay(r, g, T):
     # relative gap is 1.55e-8 (> 1e-8); the next step meets the gap (2.3e-10) and lifts pres to
     # 2.4e-8 (> 1e-8), the one after to 4.8e-5, the step then fails and ECOS backtracks to the
     # best iterate (exit 10) -- the KKT solves refine to ~1e-15 of their scale throughout.  Host
-    # build 54 of 60 agree; the highway scenes hold 90%
+    # build 54 of 60 agree, GPU 57 of 60 (profiles/r03/r03w_gpu_tests.log): the highway scenes'
+    # 90% bar holds here too
     agree = float(np.mean(r["status"] == exits))
     print(f"merge replay: exit codes agree on {agree:.3f} of {T} steps")
-    assert agree >= 0.8, (r["status"], exits)
+    assert agree >= 0.9, (r["status"], exits)
     for t in range(T):
         tight = exits[t] == 0 and r["status"][t] == 0
         rtol, atol = (1e-6, 5e-4) if tight else (1e-4, 5e-3)

@@ -29,7 +29,7 @@ cols = ["VGPRs", "AGPRs", "SGPRs", "VGPRs Spill", "SGPRs Spill", "ScratchSize [b
         "LDS Size [bytes/block]", "Occupancy [waves/SIMD]"]
 print("%-60s " % "function" + " ".join("%8s" % c.split()[0][:8] + ("" if " " not in c else "") for c in cols))
 for b, d in zip(blocks, dem):
-    d = re.sub(r"\(.*", "", d)[-60:]
+    d = re.sub(r"\(.*", "", d.replace("(anonymous namespace)::", ""))[-60:]
     print("%-60s " % d + " ".join("%8s" % b.get(c, "-") for c in cols))
 EOF
 rm -f /tmp/ru_$$.o /tmp/ru_$$.log
