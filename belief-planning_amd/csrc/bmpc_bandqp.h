@@ -108,41 +108,59 @@ BMPC_HD BandQPWs bandqp_ws(const BandQPDesc& d, double* base) {
 
 // out = K v, K the symmetric band matrix Kb with its diagonal replaced by dg.  A lane's row
 // loads are issued in chunks of 8 (band entry and vector entry, indices clamped and the extra
-// terms masked by a zero factor), so a row costs bw / 4 memory round trips instead of 2 bw;
-// the terms are added in the same order as a plain row loop (lower part, then upper part).
+// terms masked by a zero factor), two rows at a time, so two rows cost bw / 4 memory round
+// trips instead of 4 bw; each row's terms are added in the order of a plain row loop (lower
+// part, then upper part; masked terms add exact zeros).
 template <class X>
 BMPC_HD void bqp_matvec(const X& ex, const BandQPDesc& d, const double* Kb, const double* dg, const double* v,
                         double* out) {
-  const int nk = d.nk, W = d.W, bw = d.bw;
+  const int nk = d.nk, W = d.W, bw = d.bw, nl = ex.nlanes;
   constexpr int CH = 8;
   BQP_TIC(t0);
-  for (int i = ex.lane; i < nk; i += ex.nlanes) {
-    double a = dg[i] * v[i];
-    const int k0 = i < bw ? i : bw;
-    const int k1 = nk - 1 - i < bw ? nk - 1 - i : bw;
-    for (int kb = 1; kb <= k0; kb += CH) {   // row i, columns i - k
-      double e[CH], x[CH];
+  // two rows per lane per trip (i and i + nl; the second clamped to i and dropped when past
+  // nk): their chunk loads are in flight together
+  for (int i0 = ex.lane; i0 < nk; i0 += 2 * nl) {
+    const bool two = i0 + nl < nk;
+    const int ri[2] = {i0, two ? i0 + nl : i0};
+    double a[2], e[2][CH], x[2][CH];
+    int k0[2], k1[2];
 #pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const bool in = kb + u <= k0;
-        e[u] = Kb[(size_t)i * W + (in ? kb + u : 0)];
-        x[u] = v[in ? i - kb - u : i];
-      }
-#pragma unroll
-      for (int u = 0; u < CH; ++u) a += e[u] * (x[u] * (kb + u <= k0 ? 1.0 : 0.0));
+    for (int h = 0; h < 2; ++h) {
+      const int i = ri[h];
+      a[h] = dg[i] * v[i];
+      k0[h] = i < bw ? i : bw;
+      k1[h] = nk - 1 - i < bw ? nk - 1 - i : bw;
     }
-    for (int kb = 1; kb <= k1; kb += CH) {   // column i of the rows i + k below
-      double e[CH], x[CH];
+    for (int kb = 1; kb <= bw; kb += CH) {   // lower part: row i, columns i - k
 #pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const bool in = kb + u <= k1;
-        e[u] = Kb[(size_t)(in ? i + kb + u : i) * W + (in ? kb + u : 0)];
-        x[u] = v[in ? i + kb + u : i];
-      }
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int u = 0; u < CH; ++u) a += e[u] * (x[u] * (kb + u <= k1 ? 1.0 : 0.0));
+        for (int u = 0; u < CH; ++u) {
+          const bool in = kb + u <= k0[h];
+          e[h][u] = Kb[(size_t)ri[h] * W + (in ? kb + u : 0)];
+          x[h][u] = v[in ? ri[h] - kb - u : ri[h]];
+        }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int u = 0; u < CH; ++u) a[h] += e[h][u] * (x[h][u] * (kb + u <= k0[h] ? 1.0 : 0.0));
     }
-    out[i] = a;
+    for (int kb = 1; kb <= bw; kb += CH) {   // upper part: column i of the rows i + k below
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const bool in = kb + u <= k1[h];
+          e[h][u] = Kb[(size_t)(in ? ri[h] + kb + u : ri[h]) * W + (in ? kb + u : 0)];
+          x[h][u] = v[in ? ri[h] + kb + u : ri[h]];
+        }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int u = 0; u < CH; ++u) a[h] += e[h][u] * (x[h][u] * (kb + u <= k1[h] ? 1.0 : 0.0));
+    }
+    out[ri[0]] = a[0];
+    if (two) out[ri[1]] = a[1];
   }
   ex.sync();
   BQP_TOC(2, t0);
