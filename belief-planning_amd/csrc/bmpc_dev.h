@@ -48,6 +48,8 @@ struct DevExecT {
   static constexpr int nlanes = 64;
   // one wave runs a band QP: blocked factorisation and sweeps on wave broadcasts (bmpc_bandqp.h)
   static constexpr bool kBqpWave = true;
+  // small dense systems with a lane per row (bmpc_ipm.h, small_lu_solve_rows)
+  static constexpr bool kRowLanes = true;
   // lane l's v, wave-uniform (l uniform)
   __device__ double rlane(double v, int l) const {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
@@ -122,6 +124,7 @@ struct DevBlockExecT {
   ldouble* eco;
   ldouble* red;   // reduction scratch: kRedMax * NW doubles
   static constexpr int nlanes = 64 * NW;
+  static constexpr bool kRowLanes = true;
   static constexpr int kTaskLanes = 4;
   static constexpr int kConeRegRows = 8;
   static constexpr int kRedMax = 16;

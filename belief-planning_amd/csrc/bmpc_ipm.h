@@ -14,6 +14,8 @@
 // coupling system (Woodbury / Schur), solved by LU with partial pivoting.
 #pragma once
 
+#include <type_traits>
+
 #include "bmpc_tree.h"
 
 #ifndef BMPC_TS_UN
@@ -2164,19 +2166,71 @@ BMPC_FN bool small_lu(const X ex, PM* M, PP* piv, int n) {
     if (ex.lane == 0) piv[k] = (double)p;
     ex.sync();
     const double d = M[k * n + k];
-    for (int i = k + 1 + ex.lane; i < n; i += ex.nlanes) {
-      const double l = M[i * n + k] / d;
-      M[i * n + k] = l;
-      for (int j = k + 1; j < n; ++j) M[i * n + j] -= l * M[k * n + j];
-    }
+    for (int i = k + 1 + ex.lane; i < n; i += ex.nlanes) M[i * n + k] = M[i * n + k] / d;
+    ex.sync();
+    // trailing update: every entry (i, j) of rows and columns k+1.. dealt over the lanes with
+    // eight entries' loads in flight per lane (a row per lane would chain its n - k - 1
+    // read-modify-writes, a memory round trip each when the system lives in the slab); each
+    // entry gets the same single update M_ij - l_i M_kj as before
+    const int m = n - k - 1;
+    strided_batch<8>(ex.lane, ex.nlanes, m * m, [&](int t) {
+      const int i = k + 1 + t / m, j = k + 1 + t % m;
+      return M[i * n + j] - M[i * n + k] * M[k * n + j];
+    }, [&](int t, double v) { M[(k + 1 + t / m) * n + k + 1 + t % m] = v; });
     ex.sync();
   }
   return true;
 }
 
-// solve with the LU above; b in LDS, column-oriented substitution (one step per row)
+template <class X, class = void>
+struct RowLanes : std::false_type {};
+template <class X>
+struct RowLanes<X, std::void_t<decltype(X::kRowLanes)>> : std::integral_constant<bool, X::kRowLanes> {};
+
+// The substitutions with lane j owning row j (n <= lanes, device executors): each lane loads
+// its row's next eight matrix entries in one batch, so the per-row chain waits on the LDS
+// right-hand side only (the matrix is in the slab in lean launches: one dependent global load
+// per row otherwise).  Same operations in the same order as the column loops below.
 template <class X, class PM, class PB>
-BMPC_HD void small_lu_solve(const X ex, const PM* M, const PM* piv, PB* b, int n) {
+BMPC_HD void small_lu_solve_rows(const X ex, const PM* M, PB* b, int n) {
+  const int j = ex.lane;
+  const bool row = j < n;
+  const size_t rj = (size_t)(row ? j : 0) * n;
+  for (int i0 = 0; i0 < n; i0 += 8) {   // L (unit diagonal)
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i0 + u < n ? i0 + u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < n) {   // uniform
+        const double bi = b[i];
+        if (row && j > i) b[j] -= mc[u] * bi;
+        ex.sync();
+      }
+    }
+  }
+  for (int i1 = n - 1; i1 >= 0; i1 -= 8) {   // U: row i's lane divides by its diagonal first
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i1 - u >= 0 ? i1 - u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i1 - u;
+      if (i >= 0) {   // uniform
+        if (j == i) b[i] = b[i] / mc[u];
+        ex.sync();
+        const double bi = b[i];
+        if (row && j < i) b[j] -= mc[u] * bi;
+        ex.sync();
+      }
+    }
+  }
+}
+
+// solve with the LU above; b in LDS, column-oriented substitution (one step per row)
+template <class X, class PM, class PP, class PB>
+BMPC_HD void small_lu_solve(const X ex, const PM* M, const PP* piv, PB* b, int n) {
   if (ex.lane == 0)
     for (int k = 0; k < n; ++k) {
       const int p = (int)piv[k];
@@ -2187,6 +2241,12 @@ BMPC_HD void small_lu_solve(const X ex, const PM* M, const PM* piv, PB* b, int n
       }
     }
   ex.sync();
+  if constexpr (RowLanes<X>::value) {
+    if (n <= X::nlanes) {
+      small_lu_solve_rows(ex, M, b, n);
+      return;
+    }
+  }
   for (int i = 0; i < n; ++i) {          // L (unit diagonal)
     const double bi = b[i];
     for (int j = i + 1 + ex.lane; j < n; j += ex.nlanes) b[j] -= M[j * n + i] * bi;
@@ -2208,6 +2268,9 @@ BMPC_HD auto coup_mem(const X& ex, gdouble* ws, CLayout& L, CPlan& P, int off) {
   if constexpr (X::kCoupLds) return ex.lds + off;
   else return ws + L.coup + (off - P.lds_M);
 }
+// its pivots and right-hand side: LDS in every launch (Plan::lds_piv / lds_rhs precede lds_M)
+template <class X>
+BMPC_HD auto coup_vec(const X& ex, int off) { return ex.lds + off; }
 
 // global variable index -> position in the primal vector
 BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
@@ -2299,7 +2362,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
     M[(ng + nb + k) * ns + i] = -ck * gv;
   }
   ex.sync();
-  return small_lu(ex, M, coup_mem(ex, ws, L, P, P.lds_piv), ns);
+  return small_lu(ex, M, coup_vec(ex, P.lds_piv), ns);
 }
 
 template <class X, int NX, int NU, bool R3ZERO>
@@ -2340,7 +2403,7 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
   gdouble* ws = C.ws;
   gdouble* tr = ws + L.k_r0;
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
-  auto* b = coup_mem(ex, ws, L, P, P.lds_rhs);
+  auto* b = coup_vec(ex, P.lds_rhs);
   const gdouble* eta = ws + L.eta;
   if (coup_supp_dots(P)) {   // g_k' dx over each cone's support, sixteen cones per pass
     const auto t = topo_view(P, ex);
@@ -2361,7 +2424,7 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
   }
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
-  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_mem(ex, ws, L, P, P.lds_piv), b, ns);
+  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b, ns);
   const auto* bc = b + ng + nb;
   const gdouble* colk = ws + L.colk;
   const gdouble* colnu = ws + L.colnu;

@@ -50,21 +50,24 @@ BMPC_HD bool ph_flag(const X& ex, const gdouble* st, int slot) {
   return ex.uniform(st[slot] != 0.0);
 }
 
-// the factored coupling system (matrix | pivots) between kernels: LDS <-> Layout::coup
+// the factored coupling system between kernels: LDS matrix -> Layout::coup[0, nsm^2), LDS
+// pivots -> Layout::coup[nsm^2, nsm^2 + nsm)
 template <class X>
 BMPC_HD void coup_save(const X& ex, const Ctx& C) {
   CPlan& P = *C.P;
-  const int n = P.nsm * P.nsm + P.nsm;
+  const int nm = P.nsm * P.nsm, n = nm + P.nsm;
   gdouble* dst = C.ws + C.L->coup;
-  lane_batch<8>(ex, 0, n, [&](int i) { return (double)ex.lds[P.lds_M + i]; }, [&](int i, double v) { dst[i] = v; });
+  lane_batch<8>(ex, 0, n, [&](int i) { return (double)ex.lds[i < nm ? P.lds_M + i : P.lds_piv + (i - nm)]; },
+                [&](int i, double v) { dst[i] = v; });
   ex.sync();
 }
 template <class X>
 BMPC_HD void coup_load(const X& ex, const Ctx& C) {
   CPlan& P = *C.P;
-  const int n = P.nsm * P.nsm + P.nsm;
+  const int nm = P.nsm * P.nsm, n = nm + P.nsm;
   const gdouble* src = C.ws + C.L->coup;
-  lane_batch<8>(ex, 0, n, [&](int i) { return src[i]; }, [&](int i, double v) { ex.lds[P.lds_M + i] = v; });
+  lane_batch<8>(ex, 0, n, [&](int i) { return src[i]; },
+                [&](int i, double v) { ex.lds[i < nm ? P.lds_M + i : P.lds_piv + (i - nm)] = v; });
   ex.sync();
 }
 
