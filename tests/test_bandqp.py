@@ -195,3 +195,27 @@ def test_gpu_batch_and_belief_problems(gpu):
         r = gpu.qp_solve(P, q, A, l, u)
         assert r["status"][0] == 1, (name, t)
         np.testing.assert_allclose(r["x"][0], sol, atol=1e-7 * max(1, np.abs(sol).max()), err_msg=f"{name} s{t}")
+
+
+@pytest.mark.gpu
+def test_gpu_large_batch_window_path_and_cache(gpu):
+    """More problems than CUs (the factor streamed through the LDS window, in the workspace) and
+    repeated calls on one pattern (the cached analysis): solutions equal the oracle's, and a
+    call whose bounds classify the rows differently gets an analysis of its own."""
+    rng = np.random.default_rng(5)
+    P, q, A, l, u = random_qp(24, 30, 3, 4, rng)
+    B = 300
+    qs = q[None, :] + 0.1 * rng.normal(size=(B, len(q)))
+    for rep in range(2):   # the second call hits the cache
+        r = gpu.qp_solve([P] * B, qs, [A] * B, np.tile(l, (B, 1)), np.tile(u, (B, 1)))
+        assert np.all(r["status"] == 1), rep
+        for b in (0, 150, B - 1):
+            xo, _ = oracle_solve(P, qs[b], A, l, u)
+            np.testing.assert_allclose(r["x"][b], xo, atol=X_TOL * max(1, np.abs(xo).max()))
+    u2 = u.copy()
+    fin = np.where(np.isfinite(u2) & np.isfinite(l) & (u2 > l))[0]
+    u2[fin[0]] = np.inf   # a two-sided row becomes one-sided: another row class
+    r = gpu.qp_solve(P, q, A, l, u2)
+    xo, _ = oracle_solve(P, q, A, l, u2)
+    assert r["status"][0] == 1
+    np.testing.assert_allclose(r["x"][0], xo, atol=X_TOL * max(1, np.abs(xo).max()))
