@@ -113,6 +113,22 @@ def test_host_build_batch_shares_the_pattern():
         np.testing.assert_allclose(r["x"][b], xo, atol=X_TOL * max(1, np.abs(xo).max()))
 
 
+def test_host_build_window_and_in_lds_factorisations_agree():
+    """Small batches factor the band in place in LDS, batches of more problems than CUs stream it
+    through the ring window; both apply every column's updates in the same order, so a problem
+    gets the same numbers either way (the host build runs both column-at-a-time kernels)."""
+    rng = np.random.default_rng(8)
+    P, q, A, l, u = random_qp(18, 24, 3, 4, rng)
+    B = 260   # > 256 CUs of the analysis default: the window path
+    qs = q[None, :] + 0.1 * rng.normal(size=(B, len(q)))
+    big = _host(**qp_arrays([P] * B, qs, [A] * B, np.tile(l, (B, 1)), np.tile(u, (B, 1))))
+    for b in (0, 131, B - 1):
+        one = _host(**qp_arrays(P, qs[b], A, l, u))
+        assert big["status"][b] == one["status"][0] == 1
+        np.testing.assert_array_equal(big["x"][b], one["x"][0])
+        np.testing.assert_array_equal(big["iters"][b], one["iters"][0])
+
+
 def belief_problems():
     for name in ("belief_m1", "belief_m2"):
         g = golden(name)
