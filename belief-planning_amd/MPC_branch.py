@@ -153,6 +153,10 @@ class BranchMPC_CVaR:
             from bmpc.plan import BatchPlan
             self._plan = BatchPlan(self.plan_desc(), self.batch, self.device)
         rows = self.predictiveModel.policy_rows()
+        lref = getattr(self.predictiveModel, "lane_ref", None)   # psiref policies (merge ramp)
+        if lref is not None and lref is not getattr(self, "_lref", None):
+            self._plan.set_lane_ref(*lref)
+            self._lref = lref
         if rows != self._pol_rows:               # update_backup happened
             self._plan.set_policies([rows] * self.batch)
             self._pol_rows = rows
@@ -181,6 +185,9 @@ class BranchMPC_CVaR:
         transformation), Fx and bx (state constraints)."""
         if self.batch != 1:
             raise ValueError("this controller holds a batch; use solve_batch")
+        if not self._takes_transform() and (S is not None or Fx is not None or bx is not None):
+            # checked before any attribute changes: a refused call leaves the controller as it was
+            raise NotImplementedError("solve's S / Fx / bx need the CVaR controller over a highway model")
         if xRef is not None:
             self.xRef = xRef
         self.S = S

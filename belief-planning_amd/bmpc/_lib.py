@@ -24,17 +24,30 @@ class BmpcUnavailable(RuntimeError):
     """libbmpc.so (the MI355X kernels) cannot be loaded or has no usable HIP device."""
 
 
+EXPERIMENTAL = os.path.join(CSRC, "experimental")
+
+
+def _phased() -> bool:
+    """Tools-only builds with -DBMPC_WITH_PHASED add the phase-per-kernel IPM (csrc/experimental)."""
+    return "-DBMPC_WITH_PHASED" in EXTRA_FLAGS
+
+
 def sources():
     """Translation units of libbmpc.so: the C ABI + small kernels, one unit per predictive model's
     solver kernels (compiled in parallel), the host-side plan builders."""
-    return [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_k_highway.hip", "bmpc_k_highway_t.hip",
-                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_kp_highway.hip",
-                                            "bmpc_kp_highway_t.hip", "bmpc_kp_merge.hip", "bmpc_plan.cpp",
+    srcs = [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_k_highway.hip", "bmpc_k_highway_t.hip",
+                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_plan.cpp",
                                             "bmpc_qpplan.cpp")]
+    if _phased():
+        srcs += [os.path.join(EXPERIMENTAL, f) for f in ("bmpc_kp_highway.hip", "bmpc_kp_highway_t.hip",
+                                                         "bmpc_kp_merge.hip")]
+    return srcs
 
 
 def headers():
     hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if _phased():
+        hs += [os.path.join(EXPERIMENTAL, f) for f in os.listdir(EXPERIMENTAL) if f.endswith(".h")]
     return hs + [os.path.join(INCLUDE, "bmpc.h")]
 
 
@@ -54,7 +67,8 @@ def build(force: bool = False, verbose: bool = False, profile: bool = False) -> 
     from concurrent.futures import ThreadPoolExecutor
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              "-Wno-unused-value", "-Wno-unused-result", "-Wno-pass-failed",
-             *(["-DBMPC_PROFILE"] if profile else []), *EXTRA_FLAGS, "-I" + INCLUDE, "-I" + CSRC]
+             *(["-DBMPC_PROFILE"] if profile else []), *EXTRA_FLAGS, "-I" + INCLUDE, "-I" + CSRC,
+             *(["-I" + EXPERIMENTAL] if _phased() else [])]
     with tempfile.TemporaryDirectory(prefix="bmpc_build_") as tmp:
         objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in sources()]
         cmds = [[HIPCC, *flags, "-c", src, "-o", obj] for src, obj in zip(sources(), objs)]
@@ -102,6 +116,9 @@ _SIGS = {
     "bmpc_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "bmpc_timing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "bmpc_model_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 12),
+    "bmpc_model_eval_ref": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+                            + [C.c_void_p] * 12),
+    "bmpc_set_lane_ref": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "bmpc_hmm_eval": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 9),
     "bmpc_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 10),
     "bmpc_qp_solve": (C.c_int, [C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 5

@@ -11,9 +11,15 @@ CTRL_CVAR, CTRL_PROX, CTRL_QP, CTRL_ROBUST = 0, 1, 2, 3
 MODEL_HIGHWAY, MODEL_QUADRUPED, MODEL_HIGHWAY_MERGE = 0, 1, 2
 PLAN_TRANSFORM = 1      # bmpc_plan_desc.flags: solve's S / Fx / bx on a HIGHWAY CVaR plan
 POL_MAINTAIN, POL_BRAKE, POL_LC, POL_MAINTAIN_TRACKV, POL_FORWARD, POL_STOP = range(6)
+# the merge ramp's lane-reference (psiref) tracking backups (include/bmpc.h)
+POL_MAINTAIN_PSIREF, POL_MAINTAIN_TRACKV_PSIREF, POL_BRAKE_PSIREF = 6, 7, 8
+MAX_LANE_REF = 4096
 
 (INFO_T, INFO_U, INFO_BDIM, INFO_NBRANCH, INFO_NV, INFO_NEQ, INFO_NROWS, INFO_NCONES,
- INFO_LP, INFO_BATCH, INFO_WS_DOUBLES, INFO_COUNT) = range(12)
+ INFO_LP, INFO_BATCH, INFO_WS_DOUBLES, INFO_SOLVER, INFO_COUNT) = range(13)
+# solver kernels reported in INFO_SOLVER (include/bmpc.h BMPC_KERNEL_*)
+(KERNEL_NONE, KERNEL_IPM_RICH, KERNEL_IPM_LEAN, KERNEL_IPM_BLK4, KERNEL_IPM_BLK8, KERNEL_QP_RICH,
+ KERNEL_QP_LEAN) = range(7)
 
 
 class Policy(C.Structure):

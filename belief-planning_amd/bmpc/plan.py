@@ -175,6 +175,17 @@ class BatchPlan:
               "bmpc_get_tree")
         return out
 
+    def set_lane_ref(self, grid, values):
+        """The lane reference psiref(X) of the plan's *_PSIREF policies (bmpc_set_lane_ref)."""
+        g, v = (np.ascontiguousarray(np.asarray(a, np.float64).reshape(-1)) for a in (grid, values))
+        check(lib().bmpc_set_lane_ref(self._h, g.size, _p(g), _p(v)), "bmpc_set_lane_ref")
+
+    def last_kernel(self):
+        """The solver kernel the plan's last solve launched (abi.KERNEL_*, BMPC_INFO_SOLVER)."""
+        info = np.zeros(abi.INFO_COUNT, np.int32)
+        check(lib().bmpc_plan_info(self._h, _p(info)), "bmpc_plan_info")
+        return int(info[abi.INFO_SOLVER])
+
     # ---- timing ---------------------------------------------------------------------------
     PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
               "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree", "G_lp", "G_cone", "napplyG",
@@ -196,17 +207,21 @@ class BatchPlan:
         return dict(tree_ms=float(ms[0]), ipm_ms=float(ms[1]), count=int(cnt.value))
 
 
-def model_eval(desc: abi.PlanDesc, pol_rows, x, u, z, device: int = 0):
-    """Batched PredictiveModel evaluation on the GPU (parity entry)."""
+def model_eval(desc: abi.PlanDesc, pol_rows, x, u, z, device: int = 0, lane_ref=None):
+    """Batched PredictiveModel evaluation on the GPU (parity entry); lane_ref = (grid, values)
+    of the psiref policies' lane reference (bmpc_model_eval_ref)."""
     x, u, z = (np.ascontiguousarray(np.atleast_2d(np.asarray(v, np.float64))) for v in (x, u, z))
     B, n, d, m, N = x.shape[0], desc.n, desc.d, desc.m, desc.N
     out = dict(A=np.zeros((B, n, n)), B=np.zeros((B, n, d)), C=np.zeros((B, n)), xp=np.zeros((B, n)),
                p=np.zeros((B, m)), dp=np.zeros((B, m, n)), zpred=np.zeros((B, N, m * n)),
                h0=np.zeros(B), dh=np.zeros((B, n)))
     arr = abi.policy_array(pol_rows)
-    check(lib().bmpc_model_eval(context(device), C.byref(desc), arr, B, _p(x), _p(u), _p(z),
-                                *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh"))),
-          "bmpc_model_eval")
+    g, v = (None, None) if lane_ref is None else (np.ascontiguousarray(np.asarray(a, np.float64).reshape(-1))
+                                                  for a in lane_ref)
+    check(lib().bmpc_model_eval_ref(context(device), C.byref(desc), arr, 0 if g is None else g.size, _p(g), _p(v),
+                                    B, _p(x), _p(u), _p(z),
+                                    *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh"))),
+          "bmpc_model_eval_ref")
     return out
 
 

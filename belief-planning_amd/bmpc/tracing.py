@@ -27,6 +27,9 @@ class Tracer:
 class PolicySpec:
     kind: int
     params: tuple = ()
+    # psiref-tracking policies: the lane-reference interpolant (an object with grid ``g`` and
+    # values ``v``, highway_branch_dyn.LinearInterpolant) the kernels evaluate psiref(X) from
+    lane_ref: object = None
 
     def as_row(self):
         return (self.kind, self.params)
@@ -43,6 +46,20 @@ def trace(policies):
     return out
 
 
+def lane_ref_of(policies):
+    """The one lane reference the psiref policies of a policy list share, as (grid, values),
+    or None when no policy tracks one."""
+    refs = [p.lane_ref for p in policies if p.lane_ref is not None]
+    if not refs:
+        return None
+    r0 = refs[0]
+    for r in refs[1:]:
+        if r is not r0 and not (len(r.g) == len(r0.g) and (r.g == r0.g).all() and (r.v == r0.v).all()):
+            raise ValueError("the psiref policies of one model must track the same lane reference")
+    return r0.g, r0.v
+
+
 KIND_NAMES = {abi.POL_MAINTAIN: "maintain", abi.POL_BRAKE: "brake", abi.POL_LC: "lc",
               abi.POL_MAINTAIN_TRACKV: "maintain_trackV", abi.POL_FORWARD: "forward",
-              abi.POL_STOP: "stop"}
+              abi.POL_STOP: "stop", abi.POL_MAINTAIN_PSIREF: "maintain(psiref)",
+              abi.POL_MAINTAIN_TRACKV_PSIREF: "maintain_trackV(psiref)", abi.POL_BRAKE_PSIREF: "brake(psiref)"}

@@ -144,6 +144,10 @@ struct Plan {
   Topo t;
   int toff[BMPC_TOPO_N];   // offset of each table in the blob (int32 units)
   int ntab;                // blob length (int32 units); its LDS copy follows the nlds doubles
+  // lane reference of the *_PSIREF policies (bmpc_set_lane_ref): grid then values, nlref
+  // points each (device copy in the plan's Bundle; 0 = none)
+  const double* lref;
+  int nlref;
 };
 
 template <class X>

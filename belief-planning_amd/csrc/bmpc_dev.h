@@ -184,7 +184,9 @@ struct DevBlockExecT {
   __device__ void sum_n(double* v) const { reduce<0, K>(v); }
 };
 
-constexpr int kMaxSub = 8;   // sub-batch streams of the phase-per-kernel IPM
+#if defined(BMPC_WITH_PHASED)
+constexpr int kMaxSub = 8;   // sub-batch streams of the phase-per-kernel IPM (experimental/)
+#endif
 
 struct Bundle {
   Plan P;
@@ -363,16 +365,18 @@ struct SolveLaunch {
   bool rich;          // LDS-rich solver launch (choose_lds_rich)
   bool qp;            // OSQP-class controller (k_qp) instead of the CVaR IPM (k_ipm)
   hipStream_t stream;
-  // phase-per-kernel IPM (bmpc_dev_ph.h): per-iteration "egos going on" counters, their pinned
-  // read-back slot, the iteration limit
+  int nw = 4;        // small-batch launch: waves per ego (4 or 8)
+#if defined(BMPC_WITH_PHASED)
+  // phase-per-kernel IPM (experimental/bmpc_dev_ph.h, tools-only builds): per-iteration "egos
+  // going on" counters, their pinned read-back slot, the iteration limit, the sub-batch streams
   int32_t* d_count = nullptr;
   int32_t* h_count = nullptr;
   int maxit = 0;
   int ph_mode = 1;   // 1: one kernel per phase, 2: one kernel calling grouped out-of-line phases
-  int nw = 4;        // small-batch launch: waves per ego (4 or 8)
   int nsub = 1;                   // mode 1: sub-batches, one stream each
   hipStream_t* sub = nullptr;     // their streams [kMaxSub]
   hipEvent_t* sub_ev = nullptr;   // [kMaxSub + 1] fork / join events
+#endif
 };
 
 template <class M>
@@ -436,10 +440,12 @@ hipError_t launch_solver_blk_highway(const SolveLaunch& a);
 hipError_t launch_solver_blk_highway_t(const SolveLaunch& a);
 hipError_t launch_solver_blk_merge(const SolveLaunch& a);
 hipError_t launch_solver_blk_quadruped(const SolveLaunch& a);
-// the phase-per-kernel CVaR IPM (bmpc_kp_*.hip)
+#if defined(BMPC_WITH_PHASED)
+// the phase-per-kernel CVaR IPM (experimental/bmpc_kp_*.hip; tools-only builds with -DBMPC_WITH_PHASED)
 hipError_t launch_ipm_phased_highway(const SolveLaunch& a);
 hipError_t launch_ipm_phased_highway_t(const SolveLaunch& a);
 hipError_t launch_ipm_phased_merge(const SolveLaunch& a);
+#endif
 
 }  // namespace dev
 }  // namespace bmpc

@@ -7,7 +7,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -17,11 +19,13 @@
 using namespace bmpc;
 using namespace bmpc::dev;
 
+#if defined(BMPC_WITH_PHASED)
 #ifndef BMPC_IPM_PHASED_DEFAULT
 #define BMPC_IPM_PHASED_DEFAULT 0
 #endif
 #ifndef BMPC_PH_STREAMS_DEFAULT
 #define BMPC_PH_STREAMS_DEFAULT 4
+#endif
 #endif
 
 namespace {
@@ -79,15 +83,33 @@ __global__ void k_reset(double* ws, size_t stride, size_t off, const uint8_t* ma
 template <class M>
 __global__ void k_model(bmpc_plan_desc D, const bmpc_policy* pol, int B, const double* x,
                         const double* u, const double* z, double* A, double* Bm, double* C,
-                        double* xp, double* p, double* dp, double* zpred, double* h0, double* dh) {
+                        double* xp, double* p, double* dp, double* zpred, double* h0, double* dh,
+                        LaneRef R) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int n = D.n, d = D.d, m = D.m, N = D.N;
 #define OFF(ptr, k) (ptr ? ptr + (size_t)b * (k) : nullptr)
   model_eval_point<M>(D, pol + (size_t)b * m, x + b * n, u + b * d, z + b * n, OFF(A, n * n),
                       OFF(Bm, n * d), OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),
-                      OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n));
+                      OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n), R);
 #undef OFF
+}
+
+bool is_psiref(int kind) {
+  return kind == BMPC_POL_MAINTAIN_PSIREF || kind == BMPC_POL_MAINTAIN_TRACKV_PSIREF ||
+         kind == BMPC_POL_BRAKE_PSIREF;
+}
+
+// a lane reference as bmpc_model_eval_ref / bmpc_set_lane_ref take it; "" when valid
+std::string check_lane_ref(int nref, const double* grid, const double* values) {
+  if (nref == 0) return "";
+  if (nref < 2 || nref > BMPC_MAX_LANE_REF) return "lane reference: need 2 <= nref <= BMPC_MAX_LANE_REF";
+  if (!grid || !values) return "lane reference: null grid / values";
+  for (int i = 0; i + 1 < nref; ++i)
+    if (!(grid[i + 1] > grid[i])) return "lane reference: the grid must be strictly increasing";
+  for (int i = 0; i < nref; ++i)
+    if (!std::isfinite(grid[i]) || !std::isfinite(values[i])) return "lane reference: non-finite entry";
+  return "";
 }
 
 __global__ void k_hmm(int M, int m, const double* __restrict__ hc, int B, const double* xb, const double* u,
@@ -207,6 +229,10 @@ struct bmpc_ctx {
   uint64_t qclock = 0;
   GrowBuf q_in, q_ws, q_out, q_aux;
   std::vector<double> q_host;
+  // bmpc_hmm_eval / bmpc_qp_solve / bmpc_model_eval share the staging buffers, the stream and
+  // the QP cache above; ctypes releases the GIL during a call, so calls from several host
+  // threads on one context are serialised here
+  std::mutex q_mu;
   ~bmpc_ctx() {
     if (qstream) hipStreamDestroy(qstream);
   }
@@ -237,11 +263,29 @@ struct bmpc_plan {
   double t_acc[2] = {0, 0};
   int t_cnt = 0;
   bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
+  int last_kernel = BMPC_KERNEL_NONE;   // solver kernel of the last launch (BMPC_INFO_SOLVER)
+  double* d_lref = nullptr;   // lane reference of the *_PSIREF policies (grid | values)
+  bool psiref = false;        // some policy in force tracks the lane reference
+#if defined(BMPC_WITH_PHASED)
   int32_t* d_count = nullptr;   // phase-per-kernel IPM: egos going on per iteration [kMaxSub][maxit + 1]
   int32_t* h_count = nullptr;   // ... pinned read-back slots [kMaxSub]
   hipStream_t sub[kMaxSub] = {};   // ... its sub-batch streams
   hipEvent_t sub_ev[kMaxSub + 1] = {};
+#endif
 };
+
+// the plan's constants and layout, with the table and lane-reference pointers at their device
+// copies, into the device Bundle the kernels read
+static hipError_t upload_bundle(bmpc_plan* pl) {
+  Bundle hb;
+  hb.P = pl->hp.plan;
+  hb.L = pl->hp.lay;
+  HostPlan tmp = pl->hp;       // re-point the table pointers at the device copy
+  tmp.point_tables(pl->d_tables);
+  hb.P.t = tmp.plan.t;
+  hb.P.lref = pl->d_lref;
+  return hipMemcpy(pl->d_bundle, &hb, sizeof(Bundle), hipMemcpyHostToDevice);
+}
 
 extern "C" {
 
@@ -295,21 +339,16 @@ int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_
       hipMalloc(&pl->d_pol, sizeof(bmpc_policy) * (size_t)batch * P.m) != hipSuccess ||
       hipMalloc(&pl->d_in, sizeof(double) * (size_t)batch * P.n * 3) != hipSuccess ||
       hipMalloc(&pl->d_out, sizeof(double) * (size_t)batch * ((size_t)P.U * P.d + (size_t)P.T * P.n + P.nbranch + 1)) != hipSuccess ||
-      hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess ||
-      hipMalloc(&pl->d_count, sizeof(int32_t) * kMaxSub * (size_t)(P.desc.maxit + 1)) != hipSuccess ||
+      hipMalloc(&pl->d_iout, sizeof(int32_t) * (size_t)batch * 2) != hipSuccess)
+    return cleanup(fail(-12, "hipMalloc failed (out of device memory?)"));
+#if defined(BMPC_WITH_PHASED)
+  if (hipMalloc(&pl->d_count, sizeof(int32_t) * kMaxSub * (size_t)(P.desc.maxit + 1)) != hipSuccess ||
       hipHostMalloc(&pl->h_count, sizeof(int32_t) * kMaxSub) != hipSuccess)
     return cleanup(fail(-12, "hipMalloc failed (out of device memory?)"));
+#endif
   if (hipMemcpy(pl->d_tables, pl->hp.blob.data(), pl->hp.blob.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(-5, "hipMemcpy tables failed"));
-  Bundle hb;
-  hb.P = P;
-  hb.L = L;
-  {
-    HostPlan tmp = pl->hp;       // re-point the table pointers at the device copy
-    tmp.point_tables(pl->d_tables);
-    hb.P.t = tmp.plan.t;
-  }
-  if (hipMemcpy(pl->d_bundle, &hb, sizeof(Bundle), hipMemcpyHostToDevice) != hipSuccess ||
+  if (upload_bundle(pl) != hipSuccess ||
       hipMemset(pl->d_ws, 0, L.stride * (size_t)batch * sizeof(double)) != hipSuccess)
     return cleanup(fail(-5, "plan upload failed"));
   pl->h_pol.assign((size_t)batch * P.m, bmpc_policy{});
@@ -319,10 +358,12 @@ int bmpc_plan_create(bmpc_ctx* ctx, const bmpc_plan_desc* desc, int batch, bmpc_
     return cleanup(fail(-5, "hipStreamCreate failed"));
   for (auto& e : pl->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(-5, "hipEventCreate failed"));
+#if defined(BMPC_WITH_PHASED)
   for (auto& q : pl->sub)
     if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(-5, "hipStreamCreate failed"));
   for (auto& e : pl->sub_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return cleanup(fail(-5, "hipEventCreate failed"));
+#endif
   *out = pl;
   return 0;
 }
@@ -339,10 +380,12 @@ int bmpc_plan_destroy(bmpc_plan* pl) {
   hipFree(pl->d_out);
   hipFree(pl->d_iout);
   hipFree(pl->d_scratch);
-  hipFree(pl->d_count);
-  if (pl->h_count) hipHostFree(pl->h_count);
+  hipFree(pl->d_lref);
   for (auto& e : pl->ev)
     if (e) hipEventDestroy(e);
+#if defined(BMPC_WITH_PHASED)
+  hipFree(pl->d_count);
+  if (pl->h_count) hipHostFree(pl->h_count);
   for (auto& q : pl->sub)
     if (q) {
       hipStreamSynchronize(q);
@@ -350,6 +393,7 @@ int bmpc_plan_destroy(bmpc_plan* pl) {
     }
   for (auto& e : pl->sub_ev)
     if (e) hipEventDestroy(e);
+#endif
   if (pl->stream) hipStreamDestroy(pl->stream);
   delete pl;
   return 0;
@@ -369,12 +413,18 @@ int bmpc_plan_info(const bmpc_plan* pl, int32_t* info) {
   info[BMPC_INFO_LP] = P.nlp;
   info[BMPC_INFO_BATCH] = pl->batch;
   info[BMPC_INFO_WS_DOUBLES] = (int32_t)pl->hp.lay.stride;
+  info[BMPC_INFO_SOLVER] = pl->last_kernel;
   return 0;
 }
 
 int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask) {
   if (!pl || !pol) return fail(-22, "null argument");
   const int m = pl->hp.plan.m;
+  for (int e = 0; e < pl->batch; ++e)
+    for (int i = 0; i < m; ++i)
+      if ((!mask || mask[e]) && is_psiref(pol[(size_t)e * m + i].kind) &&
+          pl->hp.plan.desc.model != BMPC_MODEL_HIGHWAY_MERGE)
+        return fail(-22, "lane-reference (psiref) policies need a HIGHWAY_MERGE plan");
   HIPCHECK(hipSetDevice(pl->ctx->device));
   if (pl->pol_on_device && mask) {   // keep the device-side re-targets of unmasked egos
     HIPCHECK(hipStreamSynchronize(pl->stream));
@@ -385,6 +435,8 @@ int bmpc_set_policies(bmpc_plan* pl, const bmpc_policy* pol, const uint8_t* mask
   for (int e = 0; e < pl->batch; ++e)
     if (!mask || mask[e])
       memcpy(&pl->h_pol[(size_t)e * m], pol + (size_t)e * m, sizeof(bmpc_policy) * m);
+  pl->psiref = false;
+  for (const bmpc_policy& q : pl->h_pol) pl->psiref = pl->psiref || is_psiref(q.kind);
   HIPCHECK(hipMemcpyAsync(pl->d_pol, pl->h_pol.data(), sizeof(bmpc_policy) * pl->h_pol.size(),
                           hipMemcpyHostToDevice, pl->stream));
   HIPCHECK(hipStreamSynchronize(pl->stream));
@@ -444,11 +496,13 @@ static int fold_timing(bmpc_plan* pl) {
   return 0;
 }
 
+#if defined(BMPC_WITH_PHASED)
 // 0: monolithic k_ipm, 1: one kernel per IPM phase, 2: one kernel calling grouped phases (k_ipm_g)
 static int use_phased() {
   const char* e = getenv("BMPC_IPM_PHASED");
   return e ? atoi(e) : BMPC_IPM_PHASED_DEFAULT;
 }
+#endif
 
 static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
                         double* d_upred, double* d_xpred, double* d_bw, double* d_J,
@@ -467,19 +521,19 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     const size_t want = (size_t)atol(e);
     if (want > lds_bytes && want <= pl->ctx->lds_per_cu) lds_bytes = want;
   }
+  if (pl->psiref && P.nlref == 0)
+    return fail(-22, "the plan's policies track a lane reference: set it first (bmpc_set_lane_ref)");
   if (pl->timing && (pl->t_pending < 0 || pl->t_pending >= bmpc_plan::kTimeSlots))
     return fail(-5, "timing ring out of range (t_pending = " + std::to_string(pl->t_pending) + ")");
+  const bool qp = P.desc.controller != BMPC_CTRL_CVAR;
   SolveLaunch a{pl->d_bundle, pl->d_ws, pl->d_pol, d_x, d_z, d_xref, d_upred, d_xpred, d_bw, d_J, d_status,
-                d_iters, B, lds_bytes, tl, P.desc.controller != BMPC_CTRL_CVAR, s};
-  a.d_count = pl->d_count;
-  a.h_count = pl->h_count;
-  a.maxit = P.desc.maxit;
+                d_iters, B, lds_bytes, tl, qp, s};
+  int kernel = qp ? (tl ? BMPC_KERNEL_QP_RICH : BMPC_KERNEL_QP_LEAN) : (tl ? BMPC_KERNEL_IPM_RICH : BMPC_KERNEL_IPM_LEAN);
   hipError_t (*tree)(const SolveLaunch&) = launch_tree_quadruped;
   hipError_t (*solver)(const SolveLaunch&) = launch_solver_quadruped;
-  hipError_t (*phased)(const SolveLaunch&) = nullptr;
-  if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t, phased = launch_ipm_phased_highway_t;
-  else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway, phased = launch_ipm_phased_highway;
-  else if (merge) tree = launch_tree_merge, solver = launch_solver_merge, phased = launch_ipm_phased_merge;
+  if (hwt) tree = launch_tree_highway_t, solver = launch_solver_highway_t;
+  else if (P.desc.model == BMPC_MODEL_HIGHWAY) tree = launch_tree_highway, solver = launch_solver_highway;
+  else if (merge) tree = launch_tree_merge, solver = launch_solver_merge;
   // Small batches of the CVaR IPM: one ego per multi-wave workgroup (k_solve_blk) when the batch
   // leaves CUs idle -- 4 waves per ego, 8 for trees of BMPC_BLK_WIDE_T state nodes or more.
   // Measured at one ego (profiles/r03/r03x_blk_waves.log): N=8 NB=2 22 ms vs 30 on one wave,
@@ -493,14 +547,19 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     if (const char* e = getenv("BMPC_BLOCK_WAVES")) a.nw = atoi(e) == 8 ? 8 : 4;
     a.lds_bytes = solver_lds_bytes_blk(P, xform, a.nw);
     a.rich = true;
+    kernel = a.nw == 8 ? BMPC_KERNEL_IPM_BLK8 : BMPC_KERNEL_IPM_BLK4;
     if (hwt) solver = launch_solver_blk_highway_t;
     else if (P.desc.model == BMPC_MODEL_HIGHWAY) solver = launch_solver_blk_highway;
     else if (merge) solver = launch_solver_blk_merge;
     else solver = launch_solver_blk_quadruped;
   }
-  // large batches of the CVaR IPM: the monolithic k_ipm (mode 0), one kernel per phase
-  // (bmpc_dev_ph.h, mode 1: the factored coupling system re-read into LDS by every kernel that
-  // solves with it) or one kernel calling grouped phase functions (mode 2); BMPC_IPM_PHASED
+#if defined(BMPC_WITH_PHASED)
+  // tools-only builds: the phase-per-kernel IPM (experimental/bmpc_dev_ph.h, mode 1: the factored
+  // coupling system re-read into LDS by every kernel that solves with it) or one kernel calling
+  // grouped phase functions (mode 2/3), selected by BMPC_IPM_PHASED for large LDS-rich CVaR batches
+  a.d_count = pl->d_count;
+  a.h_count = pl->h_count;
+  a.maxit = P.desc.maxit;
   a.ph_mode = use_phased();
   a.sub = pl->sub;
   a.sub_ev = pl->sub_ev;
@@ -508,8 +567,13 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     const char* e = getenv("BMPC_PH_STREAMS");
     a.nsub = e ? atoi(e) : BMPC_PH_STREAMS_DEFAULT;
   }
-  if (phased && (blk || P.desc.controller != BMPC_CTRL_CVAR || !tl || a.ph_mode == 0)) phased = nullptr;
-  if (phased) solver = phased;
+  if (!blk && !qp && tl && a.ph_mode != 0) {
+    if (hwt) solver = launch_ipm_phased_highway_t;
+    else if (P.desc.model == BMPC_MODEL_HIGHWAY) solver = launch_ipm_phased_highway;
+    else if (merge) solver = launch_ipm_phased_merge;
+  }
+#endif
+  pl->last_kernel = kernel;
   hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
   if (pl->timing) HIPCHECK(hipEventRecord(ev[0], s));
   HIPCHECK(tree(a));
@@ -770,61 +834,120 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
                     const double* x, const double* u, const double* z, double* A, double* Bm,
                     double* C, double* xp, double* p, double* dp, double* zpred, double* h0,
                     double* dh) {
+  return bmpc_model_eval_ref(ctx, desc, policies, 0, nullptr, nullptr, B, x, u, z, A, Bm, C, xp, p, dp, zpred, h0,
+                             dh);
+}
+
+int bmpc_model_eval_ref(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy* policies, int nref,
+                        const double* grid, const double* values, int B, const double* x, const double* u,
+                        const double* z, double* A, double* Bm, double* C, double* xp, double* p, double* dp,
+                        double* zpred, double* h0, double* dh) {
   if (!ctx || !desc || !policies || !x || !u || !z || B <= 0) return fail(-22, "null argument");
+  {
+    const std::string e = check_lane_ref(nref, grid, values);
+    if (!e.empty()) return fail(-22, e);
+  }
+  for (size_t i = 0; i < (size_t)B * (desc->m > 0 ? desc->m : 0); ++i)
+    if (is_psiref(policies[i].kind) && (desc->model != BMPC_MODEL_HIGHWAY_MERGE || nref == 0))
+      return fail(-22, "lane-reference (psiref) policies need the HIGHWAY_MERGE model and a lane reference");
   const int n = desc->n, d = desc->d, m = desc->m, N = desc->N;
   if (((desc->model == BMPC_MODEL_HIGHWAY || desc->model == BMPC_MODEL_HIGHWAY_MERGE) && (n != 4 || d != 2)) ||
       (desc->model == BMPC_MODEL_QUADRUPED && (n != 3 || d != 3)) ||
       (desc->model != BMPC_MODEL_HIGHWAY && desc->model != BMPC_MODEL_HIGHWAY_MERGE &&
        desc->model != BMPC_MODEL_QUADRUPED) || m < 1 || m > BMPC_MAX_M || N < 1)
     return fail(-22, "bad model dimensions");
-  HIPCHECK(hipSetDevice(ctx->device));
+  // one packed upload (policies | x | u | z) and one packed read-back of the requested outputs,
+  // on the context's stream into its grow-only buffer: the compat environments call this once
+  // per control step, so no allocation and no device-wide synchronisation per call
   const size_t sizes[] = {(size_t)n * n, (size_t)n * d, (size_t)n, (size_t)n, (size_t)m,
                           (size_t)m * n, (size_t)N * m * n, 1, (size_t)n};
   double* hosts[] = {A, Bm, C, xp, p, dp, zpred, h0, dh};
-  size_t tot = (size_t)B * (2 * n + d);
-  for (size_t s : sizes) tot += (size_t)B * s;
-  DevBuf bbuf, bpol;
-  HIPCHECK(bbuf.alloc(tot * sizeof(double)));
-  HIPCHECK(bpol.alloc(sizeof(bmpc_policy) * (size_t)B * m));
-  double* buf = bbuf.as<double>();
-  bmpc_policy* dpol = bpol.as<bmpc_policy>();
-  HIPCHECK(hipMemcpy(dpol, policies, sizeof(bmpc_policy) * (size_t)B * m, hipMemcpyHostToDevice));
-  double* dxp = buf;
-  double* dup = dxp + (size_t)B * n;
-  double* dzp = dup + (size_t)B * d;
-  HIPCHECK(hipMemcpy(dxp, x, sizeof(double) * B * n, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(dup, u, sizeof(double) * B * d, hipMemcpyHostToDevice));
-  HIPCHECK(hipMemcpy(dzp, z, sizeof(double) * B * n, hipMemcpyHostToDevice));
-  double* dev[9];
-  double* cur = dzp + (size_t)B * n;
-  for (int i = 0; i < 9; ++i) {
-    dev[i] = hosts[i] ? cur : nullptr;
-    cur += (size_t)B * sizes[i];
+  const bool want[] = {A != nullptr, Bm != nullptr, C != nullptr, xp != nullptr, p != nullptr,
+                       dp != nullptr && p != nullptr, zpred != nullptr, h0 != nullptr, dh != nullptr && h0 != nullptr};
+  const size_t npol = ((size_t)B * m * sizeof(bmpc_policy) + sizeof(double) - 1) / sizeof(double);
+  const size_t tin = npol + (size_t)B * (2 * n + d) + 2 * (size_t)nref;
+  size_t tout = 0;
+  for (int i = 0; i < 9; ++i) tout += want[i] ? (size_t)B * sizes[i] : 0;
+  std::lock_guard<std::mutex> lock(ctx->q_mu);
+  HIPCHECK(hipSetDevice(ctx->device));
+  std::vector<double>& hv = ctx->q_host;
+  hv.resize(tin + tout);
+  memcpy(hv.data(), policies, (size_t)B * m * sizeof(bmpc_policy));
+  memcpy(hv.data() + npol, x, sizeof(double) * (size_t)B * n);
+  memcpy(hv.data() + npol + (size_t)B * n, u, sizeof(double) * (size_t)B * d);
+  memcpy(hv.data() + npol + (size_t)B * (n + d), z, sizeof(double) * (size_t)B * n);
+  if (nref) {
+    memcpy(hv.data() + npol + (size_t)B * (2 * n + d), grid, sizeof(double) * nref);
+    memcpy(hv.data() + npol + (size_t)B * (2 * n + d) + nref, values, sizeof(double) * nref);
   }
-  if (dp && !p) dev[5] = nullptr;
-  if (dh && !h0) dev[8] = nullptr;
+  HIPCHECK(ctx->q_aux.reserve((tin + tout) * sizeof(double)));
+  if (!ctx->qstream) HIPCHECK(hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking));
+  hipStream_t st = ctx->qstream;
+  double* buf = ctx->q_aux.as<double>();
+  HIPCHECK(hipMemcpyAsync(buf, hv.data(), tin * sizeof(double), hipMemcpyHostToDevice, st));
+  const bmpc_policy* dpol = reinterpret_cast<const bmpc_policy*>(buf);
+  const double* dxp = buf + npol;
+  const double* dup = dxp + (size_t)B * n;
+  const double* dzp = dup + (size_t)B * d;
+  const double* dref = dzp + (size_t)B * n;
+  const LaneRef R{nref ? dref : nullptr, nref ? dref + nref : nullptr, nref};
+  double* dev[9];
+  double* cur = buf + tin;
+  for (int i = 0; i < 9; ++i) {
+    dev[i] = want[i] ? cur : nullptr;
+    if (want[i]) cur += (size_t)B * sizes[i];
+  }
   if (desc->model == BMPC_MODEL_HIGHWAY)
-    hipLaunchKernelGGL(k_model<Highway>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
-                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+    hipLaunchKernelGGL(k_model<Highway>, dim3((B + 63) / 64), dim3(64), 0, st, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8], R);
   else if (desc->model == BMPC_MODEL_HIGHWAY_MERGE)
-    hipLaunchKernelGGL(k_model<HighwayMerge>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
-                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+    hipLaunchKernelGGL(k_model<HighwayMerge>, dim3((B + 63) / 64), dim3(64), 0, st, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8], R);
   else
-    hipLaunchKernelGGL(k_model<Quadruped>, dim3((B + 63) / 64), dim3(64), 0, 0, *desc, dpol, B, dxp, dup,
-                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8]);
+    hipLaunchKernelGGL(k_model<Quadruped>, dim3((B + 63) / 64), dim3(64), 0, st, *desc, dpol, B, dxp, dup,
+                       dzp, dev[0], dev[1], dev[2], dev[3], dev[4], dev[5], dev[6], dev[7], dev[8], R);
   HIPCHECK(hipGetLastError());
-  HIPCHECK(hipDeviceSynchronize());
+  if (tout) HIPCHECK(hipMemcpyAsync(hv.data() + tin, buf + tin, tout * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const double* o = hv.data() + tin;
   for (int i = 0; i < 9; ++i)
-    if (hosts[i] && dev[i]) HIPCHECK(hipMemcpy(hosts[i], dev[i], sizeof(double) * B * sizes[i], hipMemcpyDeviceToHost));
+    if (want[i]) {
+      memcpy(hosts[i], o, sizeof(double) * (size_t)B * sizes[i]);
+      o += (size_t)B * sizes[i];
+    }
   return 0;
 }
 
+
+int bmpc_set_lane_ref(bmpc_plan* pl, int nref, const double* grid, const double* values) {
+  if (!pl) return fail(-22, "null argument");
+  if (pl->hp.plan.desc.model != BMPC_MODEL_HIGHWAY_MERGE) return fail(-22, "lane references are for HIGHWAY_MERGE plans");
+  {
+    const std::string e = check_lane_ref(nref, grid, values);
+    if (!e.empty()) return fail(-22, e);
+  }
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  HIPCHECK(hipStreamSynchronize(pl->stream));   // no solve in flight reads the old reference
+  if (pl->user_stream) HIPCHECK(hipStreamSynchronize(pl->user_stream));
+  hipFree(pl->d_lref);
+  pl->d_lref = nullptr;
+  if (nref) {
+    HIPCHECK(hipMalloc(&pl->d_lref, sizeof(double) * 2 * (size_t)nref));
+    HIPCHECK(hipMemcpy(pl->d_lref, grid, sizeof(double) * nref, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(pl->d_lref + nref, values, sizeof(double) * nref, hipMemcpyHostToDevice));
+  }
+  pl->hp.plan.nlref = nref;
+  pl->hp.plan.lref = nullptr;   // host copy unused; upload_bundle points the device copy at d_lref
+  HIPCHECK(upload_bundle(pl));
+  return 0;
+}
 
 int bmpc_hmm_eval(bmpc_ctx* ctx, int M, int m, const double* hc, int B, const double* xb, const double* u,
                   const double* xbackup, double* xbp, double* A, double* Bm, double* C, double* h0,
                   double* Jh) {
   if (!ctx || !hc || !xb || !u || !xbackup || B <= 0) return fail(-22, "null argument");
   if (M < 1 || m < 1 || M > HMM_MAX_AGENTS || m > HMM_MAX_BACKUPS) return fail(-22, "M, m must be in 1..4");
+  std::lock_guard<std::mutex> lock(ctx->q_mu);
   HIPCHECK(hipSetDevice(ctx->device));
   const size_t nb = 4 + (size_t)M * m;
   const size_t in_sz[] = {8, (size_t)B * nb, (size_t)B * 2, (size_t)B * M * m * 4};
@@ -881,6 +1004,12 @@ int bmpc_qp_solve(bmpc_ctx* ctx, int n, int m, const int32_t* Pp, const int32_t*
                   int32_t* info) {
   if (!ctx || !q || !x || !status) return fail(-22, "null argument");
   if (n < 1 || m < 0 || batch < 1 || !Pp || !Ap) return fail(-22, "need n >= 1, m >= 0, batch >= 1 and a pattern");
+  // the column pointers are checked before they size anything (the cache key below)
+  if (Pp[0] != 0 || Ap[0] != 0) return fail(-22, "column pointers must start at 0");
+  for (int j = 0; j < n; ++j)
+    if (Pp[j + 1] < Pp[j] || Ap[j + 1] < Ap[j]) return fail(-22, "column pointers must be non-decreasing");
+  if ((Pp[n] > 0 && !Pi) || (Ap[n] > 0 && !Ai)) return fail(-22, "null row-index array");
+  std::lock_guard<std::mutex> lock(ctx->q_mu);
   // the bounds of every problem are checked on every call; the analysis is looked up by
   // pattern + row classes (bandqp_analyse validates the pattern on a miss)
   std::vector<int> cls;

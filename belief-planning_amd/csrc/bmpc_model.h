@@ -203,6 +203,40 @@ BMPC_HD S softmin2(const S& a, const S& b, double g) {
 }
 
 // ------------------------------------------------------------------------------------
+// Lane reference of the psiref-tracking backups: casadi.interpolant(name, 'linear', [grid],
+// values) (main_branch.py:78-82), linear on each grid cell, the end cells extended beyond the
+// grid.  The cell of t is the last grid point <= t, clamped to [0, n-2].
+// ------------------------------------------------------------------------------------
+struct LaneRef {
+  const double* g;   // grid (increasing), n points
+  const double* v;   // values at the grid points
+  int n;             // 0: no reference
+};
+
+BMPC_HD int lref_cell(const LaneRef& R, double t) {
+  int lo = 0, hi = R.n - 1;   // invariant: g[lo] <= t < g[hi] once clamped
+  if (!(t >= R.g[1])) return 0;
+  if (t >= R.g[R.n - 2]) return R.n - 2;
+  lo = 1;
+  hi = R.n - 2;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (R.g[mid] <= t) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// psiref(t): v_i + (t - g_i) / (g_{i+1} - g_i) * (v_{i+1} - v_i); its derivative is the cell's
+// slope (exact on each cell, as CasADi's linear plugin)
+template <class S>
+BMPC_HD S lref_eval(const LaneRef& R, const S& t) {
+  const int i = lref_cell(R, val(t));
+  const double g0 = R.g[i], g1 = R.g[i + 1], v0 = R.v[i], v1 = R.v[i + 1];
+  return (t - g0) / (g1 - g0) * (v1 - v0) + v0;
+}
+
+// ------------------------------------------------------------------------------------
 // Highway: x = (X, Y, v, psi), u = (a, r)           highway_branch_dyn.py:17-398
 // ------------------------------------------------------------------------------------
 struct Highway {
@@ -217,10 +251,24 @@ struct Highway {
     xd[3] = lift<S>(0.0) + u[1];
   }
 
-  // backup policy inputs, SX branches (:54-67, :108-119, :136-146, :80-88)
+  // backup policy inputs, SX branches (:54-67, :108-119, :136-146, :80-88); the psiref
+  // kinds follow the MX branches of the same functions (:66-77, :89-96, :122-130) with
+  // psiref(X) from the lane reference R
   template <class S>
-  BMPC_HD static void policy(const bmpc_policy& p, const S* x, S* u) {
+  BMPC_HD static void policy(const bmpc_policy& p, const S* x, S* u, const LaneRef& R = LaneRef{}) {
     switch (p.kind) {
+      case BMPC_POL_MAINTAIN_PSIREF:
+        u[0] = lift<S>(0.0);
+        u[1] = lref_eval(R, x[0]) - x[3] * p.p[0];
+        break;
+      case BMPC_POL_MAINTAIN_TRACKV_PSIREF:
+        u[0] = (p.p[1] - x[2]) * 0.5;
+        u[1] = lref_eval(R, x[0]) - x[3] * p.p[0];
+        break;
+      case BMPC_POL_BRAKE_PSIREF:
+        u[0] = softmax2(lift<S>(-5.0), -x[2], 3.0);
+        u[1] = lref_eval(R, x[0]) - x[3] * p.p[0];
+        break;
       case BMPC_POL_MAINTAIN:
         u[0] = lift<S>(0.0);
         u[1] = x[3] * (-p.p[0]);
@@ -270,7 +318,7 @@ struct Highway {
   // streamed in the same summation order as the SX graph.
   template <class S>
   BMPC_HD static S bf_traj(const double* mc, double dt, int N, const bmpc_policy& ego_pol,
-                           const bmpc_policy& obs_pol, const S* x0, const double* z0) {
+                           const bmpc_policy& obs_pol, const S* x0, const double* z0, const LaneRef& R = LaneRef{}) {
     const double s0 = mc[0] + 2.0, s1 = mc[1] + 0.2;
     const double lb = mc[1] / 2.0, ub = mc[3] * 3.6 - mc[1] / 2.0;
     S xe[4], ue[2], fe[4];
@@ -279,11 +327,11 @@ struct Highway {
     for (int i = 0; i < 4; ++i) xe[i] = x0[i], zo[i] = z0[i];
     S num = lift<S>(0.0), den = lift<S>(0.0);
     for (int k = 0; k < N; ++k) {
-      policy(ego_pol, xe, ue);
+      policy(ego_pol, xe, ue, R);
       f(xe, ue, fe);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xe[i] = xe[i] + fe[i] * dt;
-      policy(obs_pol, zo, uo);
+      policy(obs_pol, zo, uo, R);
       f(zo, uo, fo);
 #pragma unroll
       for (int i = 0; i < 4; ++i) zo[i] = zo[i] + fo[i] * dt;
@@ -295,7 +343,7 @@ struct Highway {
 #pragma unroll
     for (int i = 0; i < 4; ++i) zo[i] = z0[i];
     for (int k = 0; k < N; ++k) {
-      policy(obs_pol, zo, uo);
+      policy(obs_pol, zo, uo, R);
       f(zo, uo, fo);
 #pragma unroll
       for (int i = 0; i < 4; ++i) zo[i] = zo[i] + fo[i] * dt;
@@ -328,7 +376,7 @@ struct HighwayMerge : Highway {
 
   template <class S>
   BMPC_HD static S bf_traj(const double* mc, double dt, int N, const bmpc_policy& ego_pol,
-                           const bmpc_policy& obs_pol, const S* x0, const double* z0) {
+                           const bmpc_policy& obs_pol, const S* x0, const double* z0, const LaneRef& R = LaneRef{}) {
     const double s0 = mc[0] + 1.0, s1 = mc[1] + 0.2;
     S xe[4], ue[2], fe[4];
     double zo[4], uo[2], fo[4];
@@ -336,11 +384,11 @@ struct HighwayMerge : Highway {
     for (int i = 0; i < 4; ++i) xe[i] = x0[i], zo[i] = z0[i];
     S num = lift<S>(0.0), den = lift<S>(0.0);
     for (int k = 0; k < N; ++k) {
-      policy(ego_pol, xe, ue);
+      policy(ego_pol, xe, ue, R);
       f(xe, ue, fe);
 #pragma unroll
       for (int i = 0; i < 4; ++i) xe[i] = xe[i] + fe[i] * dt;
-      policy(obs_pol, zo, uo);
+      policy(obs_pol, zo, uo, R);
       f(zo, uo, fo);
 #pragma unroll
       for (int i = 0; i < 4; ++i) zo[i] = zo[i] + fo[i] * dt;
@@ -376,7 +424,7 @@ struct Quadruped {
   }
 
   template <class S>
-  BMPC_HD static void policy(const bmpc_policy& p, const S* x, S* u) {
+  BMPC_HD static void policy(const bmpc_policy& p, const S* x, S* u, const LaneRef& = LaneRef{}) {
     (void)x;
     u[0] = lift<S>(p.kind == BMPC_POL_FORWARD ? p.p[0] : 0.0);  // backup_forward/stop (:34-54)
     u[1] = lift<S>(0.0);
@@ -397,18 +445,18 @@ struct Quadruped {
   // BF_traj (:204-211): softmin_5 over robot_col(obs_k, ego_k)
   template <class S>
   BMPC_HD static S bf_traj(const double* mc, double dt, int N, const bmpc_policy& ego_pol,
-                           const bmpc_policy& obs_pol, const S* x0, const double* z0) {
+                           const bmpc_policy& obs_pol, const S* x0, const double* z0, const LaneRef& R = LaneRef{}) {
     S xe[3], ue[3], fe[3];
     double zo[3], uo[3], fo[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) xe[i] = x0[i], zo[i] = z0[i];
     S num = lift<S>(0.0), den = lift<S>(0.0);
     for (int k = 0; k < N; ++k) {
-      policy(ego_pol, xe, ue);
+      policy(ego_pol, xe, ue, R);
       f(xe, ue, fe);
 #pragma unroll
       for (int i = 0; i < 3; ++i) xe[i] = xe[i] + fe[i] * dt;
-      policy(obs_pol, zo, uo);
+      policy(obs_pol, zo, uo, R);
       f(zo, uo, fo);
 #pragma unroll
       for (int i = 0; i < 3; ++i) zo[i] = zo[i] + fo[i] * dt;
@@ -472,13 +520,13 @@ BMPC_HD void step(double dt, const double* x, const double* u, double* xp) {
 // zpred column block of one policy: rows x_1..x_N of propagate_backup (:174-187)
 template <class M>
 BMPC_HD void rollout(double dt, int N, const bmpc_policy& pol, const double* z0, double* out,
-                     int row_stride) {
+                     int row_stride, const LaneRef& R = LaneRef{}) {
   constexpr int NX = M::NX, NU = M::NU;
   double z[NX], u[NU], f[NX];
 #pragma unroll
   for (int i = 0; i < NX; ++i) z[i] = z0[i];
   for (int k = 0; k < N; ++k) {
-    M::policy(pol, z, u);
+    M::policy(pol, z, u, R);
     M::f(z, u, f);
 #pragma unroll
     for (int i = 0; i < NX; ++i) z[i] = z[i] + f[i] * dt;
@@ -490,7 +538,7 @@ BMPC_HD void rollout(double dt, int N, const bmpc_policy& pol, const double* z0,
 // branch_eval (:298-301): p[m] and dp[m][NX] at (x, z)
 template <class M>
 BMPC_HD void branch_eval(const double* mc, double dt, int N, int m, const bmpc_policy* pol,
-                         const double* x, const double* z, double* p, double* dp) {
+                         const double* x, const double* z, double* p, double* dp, const LaneRef& R = LaneRef{}) {
   constexpr int NX = M::NX;
   Dual<NX> xs[NX];
 #pragma unroll
@@ -498,7 +546,7 @@ BMPC_HD void branch_eval(const double* mc, double dt, int N, int m, const bmpc_p
   Dual<NX> wts[BMPC_MAX_M];
   Dual<NX> sum = dconst<NX>(0.0);
   for (int i = 0; i < m; ++i) {
-    Dual<NX> h = M::bf_traj(mc, dt, N, pol[0], pol[i], xs, z);
+    Dual<NX> h = M::bf_traj(mc, dt, N, pol[0], pol[i], xs, z, R);
     wts[i] = M::prob_weight(mc, h);
   }
   for (int i = 0; i < m; ++i) sum = sum + wts[i];

@@ -160,7 +160,7 @@ template <class M>
 BMPC_HD void model_eval_point(const bmpc_plan_desc& D, const bmpc_policy* pol, const double* x,
                               const double* u, const double* z, double* A, double* Bm, double* C,
                               double* xp, double* p, double* dp, double* zpred, double* h0,
-                              double* dh) {
+                              double* dh, const LaneRef& R = LaneRef{}) {
   constexpr int NX = M::NX, NU = M::NU;
   double tA[NX * NX], tB[NX * NU], tC[NX], txp[NX];
   linearize<M>(D.dt, x, u, tA, tB, tC, txp);
@@ -172,9 +172,9 @@ BMPC_HD void model_eval_point(const bmpc_plan_desc& D, const bmpc_policy* pol, c
     for (int i = 0; i < NX; ++i) C[i] = tC[i];
   if (xp)
     for (int i = 0; i < NX; ++i) xp[i] = txp[i];
-  if (p) branch_eval<M>(D.mc, D.dt, D.N, D.m, pol, x, z, p, dp);
+  if (p) branch_eval<M>(D.mc, D.dt, D.N, D.m, pol, x, z, p, dp, R);
   if (zpred)
-    for (int i = 0; i < D.m; ++i) rollout<M>(D.dt, D.N, pol[i], z, zpred + i * NX, D.m * NX);
+    for (int i = 0; i < D.m; ++i) rollout<M>(D.dt, D.N, pol[i], z, zpred + i * NX, D.m * NX, R);
   if (h0) col_eval<M>(D.mc, x, z, h0, dh);
 }
 

@@ -73,6 +73,7 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
   }
   ex.sync();
   // ---- BFS by depth ---------------------------------------------------------------------
+  const LaneRef R{P.lref, P.lref + P.nlref, P.nlref};   // psiref policies' lane reference
   int b0 = 0, nb = 1;   // branches of the current depth: [b0, b0+nb)
   for (int D = 0; D < P.NB; ++D) {
     // (a) branch probabilities of each non-leaf branch at this depth, and zpred blocks
@@ -81,10 +82,10 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
       const int last = t.br_ndx[b] + t.br_len[b] - 1;
       if (i < 0) {
         branch_eval<M>(mc, dt, N, m, E.pol, xbar + last * n, zbar + last * n, p + b * m,
-                       ws + L.dp + (size_t)b * m * n);   // BranchTree.dp (:1711, :1842)
+                       ws + L.dp + (size_t)b * m * n, R);   // BranchTree.dp (:1711, :1842)
       } else {
         const int c = t.br_child0[b] + i;
-        rollout<M>(dt, N, E.pol[i], zbar + last * n, zbar + t.br_ndx[c] * n, n);
+        rollout<M>(dt, N, E.pol[i], zbar + last * n, zbar + t.br_ndx[c] * n, n, R);
       }
     }
     ex.sync();

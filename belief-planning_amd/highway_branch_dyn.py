@@ -12,7 +12,7 @@ from __future__ import annotations
 import numpy as np
 
 from bmpc import abi
-from bmpc.tracing import PolicySpec, Tracer, trace
+from bmpc.tracing import PolicySpec, Tracer, lane_ref_of, trace
 
 __all__ = ["np", "dubin", "softsat", "backup_maintain", "backup_maintain_trackV", "backup_brake",
            "backup_lc", "softmin", "softmax", "propagate_backup", "lane_bdry_h", "veh_col",
@@ -41,19 +41,23 @@ def softmax(x, gamma=1):
 
 
 class PsirefPolicy(NotImplementedError):
-    """A backup policy that tracks a lane-reference interpolant (the merge ramp): not
-    lowered to a GPU descriptor (see PredictiveModel_merge)."""
+    """A backup policy whose lane reference is not a 1-D linear interpolant (the only form the
+    kernels evaluate)."""
 
 
-def _psiref_unsupported():
-    raise PsirefPolicy("psiref-tracking policies (the merge ramp's lane reference) are not lowered "
-                       "to GPU policy descriptors")
+def _lane_ref(psiref):
+    if not isinstance(psiref, LinearInterpolant):
+        raise PsirefPolicy("psiref must be a 1-D linear interpolant (interpolant(name, 'linear', [grid], values))")
+    if psiref.g.size < 2 or psiref.g.size > abi.MAX_LANE_REF or not np.all(np.diff(psiref.g) > 0):
+        raise PsirefPolicy("the lane reference's grid must be strictly increasing, 2 .. MAX_LANE_REF points")
+    return psiref
 
 
 class LinearInterpolant:
     """``casadi.interpolant(name, 'linear', [grid], values)`` for the merge scene's lane
     reference (main_branch.py:76-77, Highway_env_branch.py:312-313): piecewise linear on the
-    grid cells, the end cells extended beyond the grid (CasADi's 'linear' plugin)."""
+    grid cells, the end cells extended beyond the grid (CasADi's 'linear' plugin).  Policies
+    that track it lower to *_PSIREF descriptors; the kernels evaluate the same interpolant."""
 
     def __init__(self, name, grid, values):
         self.name = name
@@ -76,10 +80,10 @@ def interpolant(name, solver, grid, values, *opts):
 
 
 def backup_maintain(x, cons, psiref=None):
-    """Keep speed, steer psi to 0 (:54-78)."""
+    """Keep speed, steer psi to 0 (:54-78); with psiref, steer to the lane reference."""
     if isinstance(x, Tracer):
         if psiref is not None:
-            _psiref_unsupported()
+            return PolicySpec(abi.POL_MAINTAIN_PSIREF, (float(cons.Kpsi),), _lane_ref(psiref))
         return PolicySpec(abi.POL_MAINTAIN, (float(cons.Kpsi),))
     r = -cons.Kpsi * x[3] if psiref is None else psiref(x[0]) - cons.Kpsi * x[3]
     return np.array([0.0, r])
@@ -89,7 +93,7 @@ def backup_maintain_trackV(x, cons, v0, psiref=None):
     """Track speed v0 (:80-96)."""
     if isinstance(x, Tracer):
         if psiref is not None:
-            _psiref_unsupported()
+            return PolicySpec(abi.POL_MAINTAIN_TRACKV_PSIREF, (float(cons.Kpsi), float(v0)), _lane_ref(psiref))
         return PolicySpec(abi.POL_MAINTAIN_TRACKV, (float(cons.Kpsi), float(v0)))
     r = -cons.Kpsi * x[3] if psiref is None else psiref(x[0]) - cons.Kpsi * x[3]
     return np.array([0.5 * (v0 - x[2]), r])
@@ -97,10 +101,11 @@ def backup_maintain_trackV(x, cons, v0, psiref=None):
 
 def backup_brake(x, cons, psiref=None):
     """Brake.  Traced (graph) form: softmax([-7, -v], 5); NumPy form: softmax([-5, -v], 3)
-    -- the two branches of the reference differ (:117 vs :121) and both are kept."""
+    -- the two branches of the reference differ (:117 vs :121) and both are kept; the psiref
+    graph form uses softmax([-5, -v], 3) (:122-126)."""
     if isinstance(x, Tracer):
         if psiref is not None:
-            _psiref_unsupported()
+            return PolicySpec(abi.POL_BRAKE_PSIREF, (float(cons.Kpsi),), _lane_ref(psiref))
         return PolicySpec(abi.POL_BRAKE, (float(cons.Kpsi),))
     r = -cons.Kpsi * x[3] if psiref is None else psiref(x[0]) - cons.Kpsi * x[3]
     return np.array([softmax(np.array([-5.0, -x[2]]), 3), r])
@@ -217,17 +222,15 @@ class PredictiveModel:
 
 class PredictiveModel_merge(PredictiveModel):
     """``highway_branch_dyn.PredictiveModel_merge`` (:400-502): the highway model whose
-    ``BF_traj`` is softmin_5 of veh_col(obstacle, ego, [L+1, W+0.2]) only (:463-467).
+    ``BF_traj`` is softmin_5 of veh_col(obstacle, ego, [L+1, W+0.2]) only (:463-467), model
+    kind HIGHWAY_MERGE (its plans take the per-solve S / bx of ``BranchMPC_CVaR.solve``).
 
-    With plain policies -- the merge scene's controller model, ``pred_model[0]`` of
-    ``main_branch.sim_merge`` (maintain_trackV(v0), brake) -- it runs on the GPU (model kind
-    HIGHWAY_MERGE; its plans take the per-solve S / bx of ``BranchMPC_CVaR.solve``).  With
-    policies that track the ramp's lane reference (``psiref``, ``pred_model[1]``) the scene
-    only asks it for the ego's own backup rollouts (``zpred_eval``, recorded by the env,
-    ``Highway_env_branch.py:331``); those rollouts are evaluated from the policies' NumPy
-    branches (same expressions as the MX branches the reference compiles: maintain_trackV
-    [0.5(v0 - v), psiref(X) - Kpsi psi], brake [softmax([-5, -v], 3), psiref(X) - Kpsi psi]),
-    and such a model cannot drive a controller."""
+    Both of the merge scene's models run on the GPU: ``pred_model[0]`` (maintain_trackV(v0),
+    brake -- the controller's model, main_branch.py:84-88) and ``pred_model[1]`` whose backups
+    track the ramp's lane reference (psiref, :82-85; the scene asks it for the ramp vehicles'
+    rollouts, Highway_env_branch.py:331): its policies lower to *_PSIREF descriptors and the
+    kernels evaluate psiref(X) from the interpolant's grid (bmpc_model_eval_ref; a controller
+    plan over it gets the reference through bmpc_set_lane_ref)."""
 
     model_kind = abi.MODEL_HIGHWAY_MERGE
 
@@ -242,43 +245,13 @@ class PredictiveModel_merge(PredictiveModel):
         self.update_backup(backupcons)
 
     def update_backup(self, backupcons):
-        self.backupcons = backupcons
-        self.m = len(backupcons)
-        try:
-            self.policies = trace(backupcons)
-            self.host_rollouts = False
-        except PsirefPolicy:
-            self.policies = None
-            self.host_rollouts = True
-
-    def policy_rows(self):
-        if self.host_rollouts:
-            raise PsirefPolicy("a PredictiveModel_merge with psiref policies cannot drive a controller")
-        return super().policy_rows()
+        super().update_backup(backupcons)
+        self.lane_ref = lane_ref_of(self.policies)
 
     def _eval(self, x, u, z):
-        if self.host_rollouts:     # dynamics / collision rows do not depend on the policies
-            x = np.atleast_2d(np.asarray(x, float))
-            rows = [[(abi.POL_MAINTAIN, (float(self.cons.Kpsi),))] * self.m] * x.shape[0]
-            from bmpc import plan
-            B = x.shape[0]
-            u = np.zeros((B, self.d)) if u is None else np.broadcast_to(np.atleast_2d(u), (B, self.d))
-            z = x if z is None else np.broadcast_to(np.atleast_2d(np.asarray(z, float)), (B, self.n))
-            return plan.model_eval(self.desc(), rows, x, u, z)
-        return super()._eval(x, u, z)
-
-    def branch_eval(self, x, z):
-        if self.host_rollouts:
-            raise PsirefPolicy("branch probabilities of psiref policies are not built (the scene never asks)")
-        return super().branch_eval(x, z)
-
-    def zpred_eval(self, z):
-        if not self.host_rollouts:
-            return super().zpred_eval(z)
-        z = np.asarray(z, float)
-        one = z.ndim == 1
-        out = []
-        for zz in np.atleast_2d(z):
-            cols = [propagate_backup(zz, lambda v, f=f: dubin(v, f(v)), self.N, self.dt) for f in self.backupcons]
-            out.append(np.hstack(cols))
-        return out[0] if one else np.array(out)
+        from bmpc import plan
+        x = np.atleast_2d(np.asarray(x, float))
+        B = x.shape[0]
+        u = np.zeros((B, self.d)) if u is None else np.broadcast_to(np.atleast_2d(u), (B, self.d))
+        z = x if z is None else np.broadcast_to(np.atleast_2d(np.asarray(z, float)), (B, self.n))
+        return plan.model_eval(self.desc(), [self.policy_rows()] * B, x, u, z, lane_ref=self.lane_ref)

@@ -82,8 +82,18 @@ enum {
   BMPC_POL_LC = 2,              /* backup_lc(x,x0)                  p = x0[0..3]        */
   BMPC_POL_MAINTAIN_TRACKV = 3, /* backup_maintain_trackV(x,cons,v0) p = {Kpsi, v0}     */
   BMPC_POL_FORWARD = 4,         /* quadruped backup_forward(x,v0)   p = {v0}            */
-  BMPC_POL_STOP = 5             /* quadruped backup_stop(x)                             */
+  BMPC_POL_STOP = 5,            /* quadruped backup_stop(x)                             */
+  /* the merge ramp's lane-reference tracking backups: the same policies with the psiref
+   * argument, psiref(X) = the plan's lane reference (bmpc_set_lane_ref; bmpc_model_eval_ref),
+   * a 1-D linear interpolant (casadi.interpolant 'linear', main_branch.py:78-82);
+   * highway_branch_dyn.py:54-130 MX branches.  HIGHWAY_MERGE plans only.                 */
+  BMPC_POL_MAINTAIN_PSIREF = 6,        /* u = [0, psiref(X) - Kpsi psi]            p = {Kpsi}     */
+  BMPC_POL_MAINTAIN_TRACKV_PSIREF = 7, /* u = [0.5 (v0 - v), psiref(X) - Kpsi psi] p = {Kpsi, v0} */
+  BMPC_POL_BRAKE_PSIREF = 8            /* u = [softmax([-5, -v], 3), psiref(X) - Kpsi psi]  p = {Kpsi} */
 };
+
+/* largest lane reference (grid points) a plan or bmpc_model_eval_ref takes */
+#define BMPC_MAX_LANE_REF 4096
 
 typedef struct {
   int32_t kind;
@@ -144,7 +154,19 @@ enum {
   BMPC_INFO_LP,         /* LP rows (dims['l'])                   */
   BMPC_INFO_BATCH,
   BMPC_INFO_WS_DOUBLES, /* per-ego HBM workspace slab (doubles)  */
+  BMPC_INFO_SOLVER,     /* solver kernel of the plan's last solve (BMPC_KERNEL_*)      */
   BMPC_INFO_COUNT
+};
+
+/* solver kernels (BMPC_INFO_SOLVER): which launch path the last solve took */
+enum {
+  BMPC_KERNEL_NONE = 0,      /* no solve yet                                              */
+  BMPC_KERNEL_IPM_RICH = 1,  /* k_ipm, one wave per ego, topology + coupling system in LDS */
+  BMPC_KERNEL_IPM_LEAN = 2,  /* k_ipm, one wave per ego, coupling system in the slab       */
+  BMPC_KERNEL_IPM_BLK4 = 3,  /* k_solve_blk, one ego per 4-wave workgroup (small batches)  */
+  BMPC_KERNEL_IPM_BLK8 = 4,  /* k_solve_blk, one ego per 8-wave workgroup (small batches)  */
+  BMPC_KERNEL_QP_RICH = 5,   /* k_qp (OSQP-class controllers), LDS-rich                    */
+  BMPC_KERNEL_QP_LEAN = 6    /* k_qp, lean                                                 */
 };
 
 const char* bmpc_last_error(void);
@@ -255,6 +277,23 @@ int bmpc_model_eval(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy
                     int B, const double* x, const double* u, const double* z,
                     double* A, double* Bm, double* C, double* xp, double* p, double* dp,
                     double* zpred, double* h0, double* dh);
+
+/* bmpc_model_eval for models whose policies track a lane reference (BMPC_POL_*_PSIREF):
+ * the reference psiref(X) is the linear interpolant of values [nref] over the increasing grid
+ * [nref] (2 <= nref <= BMPC_MAX_LANE_REF; outside the grid the end cells extend linearly, as
+ * casadi.interpolant 'linear' does).  Replaces PredictiveModel_merge's MX graphs with psiref
+ * backups (highway_branch_dyn.py:400-502; the merge scene's pred_model[1], main_branch.py:85,
+ * whose zpred_eval the scene calls, Highway_env_branch.py:331).  nref = 0: no reference (then
+ * no policy may be a *_PSIREF kind). */
+int bmpc_model_eval_ref(bmpc_ctx* ctx, const bmpc_plan_desc* desc, const bmpc_policy* policies,
+                        int nref, const double* grid, const double* values,
+                        int B, const double* x, const double* u, const double* z,
+                        double* A, double* Bm, double* C, double* xp, double* p, double* dp,
+                        double* zpred, double* h0, double* dh);
+
+/* The lane reference of a HIGHWAY_MERGE plan's *_PSIREF policies (same form as
+ * bmpc_model_eval_ref): shared by every ego of the plan, kept until the next call. */
+int bmpc_set_lane_ref(bmpc_plan* plan, int nref, const double* grid, const double* values);
 
 /* Closed-loop sim_overtake scene on the device, one scene per ego of a highway plan:
  * replaces Highway_env_branch.Highway_env.step (Highway_env_branch.py:83-184) around the

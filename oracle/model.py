@@ -151,12 +151,30 @@ def softsat(x, s):
 # policies: descriptor = (kind, params)
 # ---------------------------------------------------------------------------------------
 MAINTAIN, BRAKE, LC, MAINTAIN_TRACKV, FORWARD, STOP = 0, 1, 2, 3, 4, 5
+MAINTAIN_PSIREF, MAINTAIN_TRACKV_PSIREF, BRAKE_PSIREF = 6, 7, 8
 
 
 @dataclass(frozen=True)
 class Policy:
     kind: int
     params: tuple = ()
+    lane_ref: object = None     # psiref kinds: LaneRef
+
+
+class LaneRef:
+    """``casadi.interpolant(name, 'linear', [grid], values)`` (main_branch.py:78-79): linear on
+    the cell [g_i, g_i+1) holding t (the last grid point <= t, clamped to the first / last
+    cell, so the end cells extend beyond the grid); d/dt = the cell's slope."""
+
+    def __init__(self, grid, values):
+        self.g = np.asarray(grid, float).reshape(-1)
+        self.v = np.asarray(values, float).reshape(-1)
+
+    def __call__(self, t):
+        tv = _val(t)
+        i = int(np.clip(np.searchsorted(self.g, tv, side="right") - 1, 0, self.g.size - 2))
+        g0, g1, v0, v1 = self.g[i], self.g[i + 1], self.v[i], self.v[i + 1]
+        return (t - g0) / (g1 - g0) * (v1 - v0) + v0
 
 
 def policy_u(pol: Policy, x):
@@ -167,8 +185,16 @@ def policy_u(pol: Policy, x):
     * LC        -- ``backup_lc`` :136-146       u=[-0.8558(v-v*), -0.3162(y-y*)-3.9889(psi-psi*)]
     * MAINTAIN_TRACKV -- ``backup_maintain_trackV`` :80-88 u=[0.5(v0-v), -Kpsi*psi]
     * FORWARD/STOP -- ``quadruped_branch_dyn.backup_forward/stop`` :34-54
+    * *_PSIREF -- the MX branches with psiref (:66-77, :89-96, :122-130): the second input is
+      psiref(X) - Kpsi*psi, brake's first softmax([-5,-v],3)
     """
     k, p = pol.kind, pol.params
+    if k == MAINTAIN_PSIREF:
+        return [0.0, pol.lane_ref(x[0]) - x[3] * p[0]]
+    if k == MAINTAIN_TRACKV_PSIREF:
+        return [0.5 * (p[1] - x[2]), pol.lane_ref(x[0]) - x[3] * p[0]]
+    if k == BRAKE_PSIREF:
+        return [softmax([-5.0, -x[2]], 3.0), pol.lane_ref(x[0]) - x[3] * p[0]]
     if k == MAINTAIN:
         return [0.0, -p[0] * x[3]]
     if k == BRAKE:
@@ -323,11 +349,11 @@ class HighwayModel(_ModelBase):
 
 
 class HighwayMergeModel(HighwayModel):
-    """``highway_branch_dyn.PredictiveModel_merge`` (highway_branch_dyn.py:400-502) as the merge
-    scene's controller uses it (``pred_model[0]``, main_branch.py:85-88: maintain_trackV(v0) /
-    brake, no psiref): same dynamics, policies, collision row and branch probabilities as
-    the highway model; ``BF_traj`` (:463-467) is softmin_5 over veh_col(obs, ego, [L+1, W+0.2])
-    only -- no lane-boundary term."""
+    """``highway_branch_dyn.PredictiveModel_merge`` (highway_branch_dyn.py:400-502): same
+    dynamics, collision row and branch probabilities as the highway model; ``BF_traj``
+    (:463-467) is softmin_5 over veh_col(obs, ego, [L+1, W+0.2]) only -- no lane-boundary term.
+    Its policies are the merge scene's (main_branch.py:82-85): maintain_trackV(v0) / brake
+    (pred_model[0]) or their lane-reference tracking forms (*_PSIREF, pred_model[1])."""
 
     def bf_traj(self, x2, x1):
         size = [self.L + 1.0, self.W + 0.2]

@@ -68,6 +68,7 @@ struct HS {
   int batch;
   std::vector<double> ws;
   std::vector<bmpc_policy> pol;
+  std::vector<double> lref;   // lane reference (grid | values) of the psiref policies
 };
 thread_local std::string g_err;
 }  // namespace
@@ -109,6 +110,7 @@ int hs_info(void* p, int32_t* info) {
   info[BMPC_INFO_LP] = P.nlp;
   info[BMPC_INFO_BATCH] = h->batch;
   info[BMPC_INFO_WS_DOUBLES] = (int32_t)h->hp.lay.stride;
+  info[BMPC_INFO_SOLVER] = BMPC_KERNEL_NONE;   // the host build has no kernels
   return 0;
 }
 
@@ -267,6 +269,41 @@ int hs_get_tree(void* p, double* xbar, double* ubar, double* zbar, double* w, do
     if (w) memcpy(w + (size_t)e * P.nbranch, ws + L.w, sizeof(double) * P.nbranch);
     if (pr) memcpy(pr + (size_t)e * P.bdim * P.m, ws + L.p, sizeof(double) * P.bdim * P.m);
     if (sol) memcpy(sol + (size_t)e * P.nv, ws + L.sol, sizeof(double) * P.nv);
+  }
+  return 0;
+}
+
+int hs_set_lane_ref(void* hp, int nref, const double* grid, const double* values) {
+  HS* h = (HS*)hp;
+  h->lref.assign(grid, grid + nref);
+  h->lref.insert(h->lref.end(), values, values + nref);
+  h->hp.plan.lref = nref ? h->lref.data() : nullptr;
+  h->hp.plan.nlref = nref;
+  return 0;
+}
+
+int hs_model_eval_ref(const bmpc_plan_desc* D, const bmpc_policy* pol, int nref, const double* grid,
+                      const double* values, int B, const double* x, const double* u, const double* z, double* A,
+                      double* Bm, double* C, double* xp, double* p, double* dp, double* zpred, double* h0,
+                      double* dh) {
+  const int n = D->n, d = D->d, m = D->m, N = D->N;
+  const LaneRef R{grid, values, nref};
+  for (int b = 0; b < B; ++b) {
+    const bmpc_policy* pb = pol + (size_t)b * m;
+#define OFF(ptr, k) (ptr ? ptr + (size_t)b * (k) : nullptr)
+    if (D->model == BMPC_MODEL_HIGHWAY)
+      model_eval_point<Highway>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n), OFF(zpred, N * m * n),
+                                OFF(h0, 1), OFF(dh, n), R);
+    else if (D->model == BMPC_MODEL_HIGHWAY_MERGE)
+      model_eval_point<HighwayMerge>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                     OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n), OFF(zpred, N * m * n),
+                                     OFF(h0, 1), OFF(dh, n), R);
+    else
+      model_eval_point<Quadruped>(*D, pb, x + b * n, u + b * d, z + b * n, OFF(A, n * n), OFF(Bm, n * d),
+                                  OFF(C, n), OFF(xp, n), OFF(p, m), OFF(dp, m * n),
+                                  OFF(zpred, N * m * n), OFF(h0, 1), OFF(dh, n), R);
+#undef OFF
   }
   return 0;
 }

@@ -26,7 +26,9 @@ SO = os.path.join(HERE, "hostsim", "libbmpc_hostsim%s.so" % (
     "" if not FLAGS else "_" + "".join(c if c.isalnum() else "_" for c in "".join(FLAGS))[:80]))
 SRCS = [os.path.join(HERE, "hostsim", "hostsim.cpp"), os.path.join(PKG, "csrc", "bmpc_plan.cpp"),
         os.path.join(PKG, "csrc", "bmpc_qpplan.cpp")]
-HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")]
+EXP = os.path.join(PKG, "csrc", "experimental")   # the phase sequence of the experimental phased IPM
+HDRS = [os.path.join(PKG, "csrc", f) for f in os.listdir(os.path.join(PKG, "csrc")) if f.endswith(".h")] + \
+    [os.path.join(EXP, f) for f in os.listdir(EXP) if f.endswith(".h")]
 
 
 def source_hash():
@@ -48,7 +50,8 @@ def build(force=False):
     if force or have != want:
         tmp = SO + f".{os.getpid()}.tmp"
         cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fopenmp", "-Wno-unknown-pragmas",
-               *FLAGS, "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), *SRCS, "-o", tmp]
+               *FLAGS, "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), "-I" + EXP, *SRCS,
+               "-o", tmp]
         subprocess.check_call(cmd)
         os.replace(tmp, SO)                      # atomic: concurrent test workers each build their own
         with open(stamp + f".{os.getpid()}", "w") as f:
@@ -95,6 +98,10 @@ class HostSim:
     def set_policies(self, pol_rows):
         arr = abi.policy_array(pol_rows)
         lib().hs_set_policies(self.h, arr)
+
+    def set_lane_ref(self, grid, values):
+        self._lref = [np.ascontiguousarray(np.asarray(v, float).reshape(-1)) for v in (grid, values)]
+        lib().hs_set_lane_ref(self.h, self._lref[0].size, _p(self._lref[0]), _p(self._lref[1]))
 
     def solve(self, x, z, xref):
         B, n, d = self.batch, self.desc.n, self.desc.d
@@ -182,15 +189,18 @@ class HostSim:
         return out
 
 
-def model_eval(desc, pol_rows, x, u, z):
+def model_eval(desc, pol_rows, x, u, z, lane_ref=None):
+    """Host build of bmpc_model_eval(_ref); lane_ref = (grid, values) of psiref policies."""
     x, u, z = (np.ascontiguousarray(np.atleast_2d(np.asarray(v, float))) for v in (x, u, z))
     B, n, d, m, N = x.shape[0], desc.n, desc.d, desc.m, desc.N
     out = dict(A=np.zeros((B, n, n)), B=np.zeros((B, n, d)), C=np.zeros((B, n)), xp=np.zeros((B, n)),
                p=np.zeros((B, m)), dp=np.zeros((B, m, n)), zpred=np.zeros((B, N, m * n)),
                h0=np.zeros(B), dh=np.zeros((B, n)))
     arr = abi.policy_array(pol_rows)
-    lib().hs_model_eval(C.byref(desc), arr, B, _p(x), _p(u), _p(z),
-                        *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")))
+    g, v = (None, None) if lane_ref is None else (np.ascontiguousarray(np.asarray(a, float).reshape(-1))
+                                                  for a in lane_ref)
+    lib().hs_model_eval_ref(C.byref(desc), arr, 0 if g is None else g.size, _p(g), _p(v), B, _p(x), _p(u), _p(z),
+                            *(_p(out[k]) for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")))
     return out
 
 

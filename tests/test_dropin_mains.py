@@ -47,13 +47,17 @@ class _HostPlan:
     def branch_dp(self):
         return self._hs.branch_dp()
 
+    def set_lane_ref(self, grid, values):
+        self._hs.set_lane_ref(grid, values)
+
 
 @pytest.fixture
 def host_device(monkeypatch):
     import hostsim_lib
     from bmpc import plan
     monkeypatch.setattr(plan, "BatchPlan", _HostPlan)
-    monkeypatch.setattr(plan, "model_eval", lambda desc, rows, x, u, z, device=0: hostsim_lib.model_eval(desc, rows, x, u, z))
+    monkeypatch.setattr(plan, "model_eval", lambda desc, rows, x, u, z, device=0, lane_ref=None:
+                        hostsim_lib.model_eval(desc, rows, x, u, z, lane_ref=lane_ref))
     _HostPlan.solves = 0
     yield
 

@@ -66,7 +66,7 @@ def test_device_env_replays_reference_loop(name, steps):
     assert bool(scene[0, abi.ENV_COLL].item()) == bool(g["traj_collision"][steps - 1])
 
 
-def test_device_closed_loop_follows_reference():
+def test_device_closed_loop_follows_reference(solver_path):
     """env -> solve on the device for 20 steps from the sim_overtake start (highway_n20_nb1
     recording: N=20, NB=1, the metric configuration)."""
     torch = _torch()
@@ -98,6 +98,8 @@ def test_device_closed_loop_follows_reference():
         pl.solve_device(x.data_ptr(), z.data_ptr(), xr.data_ptr(), up.data_ptr(), None, None, J.data_ptr(),
                         st.data_ptr(), it.data_ptr(), s)
     torch.cuda.synchronize()
+    from conftest import assert_solver_path
+    assert_solver_path(pl, solver_path)
     for t in range(T):
         np.testing.assert_allclose(xs[t], np.repeat(np.asarray(g["traj_x"][t])[None], B, 0), rtol=0, atol=1e-4,
                                    err_msg=f"closed-loop x at step {t}")

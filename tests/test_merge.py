@@ -195,7 +195,8 @@ def gpu():
 
 
 @pytest.mark.gpu
-def test_gpu_replays_merge_scene(gpu):
+def test_gpu_replays_merge_scene(gpu, solver_path):
+    from conftest import assert_solver_path
     g = golden(NAME)
     rb = replay_inputs(g)
     pl = gpu.BatchPlan(merge_desc(g), rb["T"])
@@ -203,6 +204,7 @@ def test_gpu_replays_merge_scene(gpu):
     pl.set_warm_start(rb["uLin"], rb["p"], rb["jcons"], mask=rb["warm"])
     pl.set_transform(rb["S"], rb["bx"])
     r = pl.solve(rb["x"], rb["z"], rb["xref"])
+    assert_solver_path(pl, solver_path)
     check_merge_replay(r, g, rb["T"])
 
 
@@ -220,3 +222,124 @@ def test_gpu_merge_model_matches_reference_code(gpu):
         out = gpu.model_eval(desc, rows, g[p + "x"], g[p + "u"], g[p + "z"])
         for key in KEYS:
             close(out[key], g[p + key], f"gpu merge {p}{key}")
+
+
+# ---- the ramp's lane-reference (psiref) policies: sim_merge's pred_model[1] ----------------------
+PSIREF = "model_merge_psiref"
+
+
+def psiref_rows(g, B):
+    v0 = float(g["v0"])
+    return [[(abi.POL_MAINTAIN_TRACKV_PSIREF, (float(g["Kpsi"]), v0)),
+             (abi.POL_BRAKE_PSIREF, (float(g["Kpsi"]),))]] * B
+
+
+def psiref_desc(N):
+    return abi.make_desc(abi.CTRL_CVAR, abi.MODEL_HIGHWAY_MERGE, 4, 2, N, 1, 2, 0.1, np.eye(4), np.eye(2),
+                         np.zeros((0, 4)), [], np.zeros((0, 2)), [], [0, 0], [4.0, 2.5, 2.0, 2.0])
+
+
+def test_psiref_merge_model_matches_reference_code():
+    """PredictiveModel_merge with the ramp's psiref-tracking backups (maintain_trackV(v0,
+    refpsi), brake(refpsi); main_branch.py:82-85) over the reference's merge_geometry lane
+    reference: vectors of the reference's own code (tools/gen_golden_model.py) against the
+    oracle restatement and the host build of the kernels' model (bmpc_model_eval_ref), 1e-12;
+    points before / after the grid and on a grid node included."""
+    import hostsim_lib as H
+    from oracle.model import BRAKE_PSIREF, MAINTAIN_TRACKV_PSIREF, HighwayMergeModel, LaneRef, Policy
+    from test_model_golden import KEYS, close
+    g = golden(PSIREF)
+    lr = LaneRef(g["grid"], g["refpsi"])
+    for c in range(int(g["ncases"])):
+        p = f"c{c}_"
+        N = int(g[p + "N"])
+        mdl = HighwayMergeModel(N, float(g["dt"]), [Policy(MAINTAIN_TRACKV_PSIREF, (0.1, float(g["v0"])), lr),
+                                                    Policy(BRAKE_PSIREF, (0.1,), lr)],
+                                L=float(g["L"]), W=float(g["W"]), s1=float(g["s1"]))
+        for k in range(g[p + "x"].shape[0]):
+            x, z, u = g[p + "x"][k], g[p + "z"][k], g[p + "u"][k]
+            got = dict(zip(("A", "B", "C", "xp"), mdl.dyn_linearization(x, u)))
+            got["p"], got["dp"] = mdl.branch_eval(x, z)
+            got["zpred"] = mdl.zpred_eval(z)
+            got["h0"], got["dh"] = mdl.col_eval(x, z)
+            for key in KEYS:
+                close(got[key], g[p + key][k], f"oracle psiref {p}{key}[{k}]")
+        B = g[p + "x"].shape[0]
+        out = H.model_eval(psiref_desc(N), psiref_rows(g, B), g[p + "x"], g[p + "u"], g[p + "z"],
+                           lane_ref=(g["grid"], g["refpsi"]))
+        for key in KEYS:
+            close(out[key], g[p + key], f"hostsim psiref {p}{key}")
+
+
+def test_compat_traces_psiref_policies():
+    """The drop-in PredictiveModel_merge lowers the reference's psiref lambdas to *_PSIREF
+    descriptors sharing the interpolant it is given (no host rollouts)."""
+    from highway_branch_dyn import PredictiveModel_merge, backup_brake, backup_maintain_trackV, interpolant
+    from utils import Branch_constants
+    g = golden(PSIREF)
+    cons = Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=7.0, rm=0.3, J_c=20, s_c=1,
+                            ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    refY = interpolant("refY", "linear", [g["grid"]], g["refY"])
+    refpsi = interpolant("refpsi", "linear", [g["grid"]], g["refpsi"])
+    v0 = float(g["v0"])
+    mdl = PredictiveModel_merge(4, 2, 40, [lambda x: backup_maintain_trackV(x, cons, v0, refpsi),
+                                           lambda x: backup_brake(x, cons, refpsi)], 0.1, cons, (refY, refpsi),
+                                laneID=1, N_lane1=2, N_lane2=1)
+    assert [k for k, _ in mdl.policy_rows()] == [abi.POL_MAINTAIN_TRACKV_PSIREF, abi.POL_BRAKE_PSIREF]
+    np.testing.assert_array_equal(mdl.lane_ref[0], g["grid"])
+    np.testing.assert_array_equal(mdl.lane_ref[1], g["refpsi"])
+
+
+def _psiref_tree_check(tree, g, p, B):
+    """The tree a solve builds at its first (inittree) step: the root branch's probabilities are
+    branch_eval(x, z) and each leaf's obstacle trajectory is zpred_eval(z)'s column block
+    (MPC_branch.py:1694-1724)."""
+    from test_model_golden import close
+    N = int(g[p + "N"])
+    close(tree["p"][:, 0, :], g[p + "p"][:B], f"tree p {p}")
+    for i in range(2):
+        zb = tree["zbar"][:, 1 + i * (N + 1):1 + i * (N + 1) + N, :]
+        close(zb, g[p + "zpred"][:B, :, 4 * i:4 * i + 4], f"tree zbar leaf {i} {p}")
+
+
+def _psiref_plan_inputs(g, p):
+    x, z = g[p + "x"], g[p + "z"]
+    xref = np.stack([np.zeros(len(x)), x[:, 1], np.full(len(x), 20.0), x[:, 3]], 1)
+    return x, z, xref
+
+
+def test_host_build_tree_with_psiref_policies():
+    """A HIGHWAY_MERGE plan whose policies track the lane reference (bmpc_set_lane_ref): the
+    host build of k_tree builds the reference's tree from them."""
+    import hostsim_lib as H
+    g = golden(PSIREF)
+    for c in range(int(g["ncases"])):
+        p = f"c{c}_"
+        B = g[p + "x"].shape[0]
+        hs = H.HostSim(psiref_desc(int(g[p + "N"])), B)
+        hs.set_policies(psiref_rows(g, B))
+        hs.set_lane_ref(g["grid"], g["refpsi"])
+        hs.solve(*_psiref_plan_inputs(g, p))
+        _psiref_tree_check(hs.tree(), g, p, B)
+
+
+@pytest.mark.gpu
+def test_gpu_psiref_merge_model_matches_reference_code(gpu):
+    """k_model (bmpc_model_eval_ref) and k_tree (a plan with bmpc_set_lane_ref) on the GPU
+    against the reference's psiref vectors, 1e-12."""
+    from test_model_golden import KEYS, close
+    g = golden(PSIREF)
+    for c in range(int(g["ncases"])):
+        p = f"c{c}_"
+        N, B = int(g[p + "N"]), g[p + "x"].shape[0]
+        out = gpu.model_eval(psiref_desc(N), psiref_rows(g, B), g[p + "x"], g[p + "u"], g[p + "z"],
+                             lane_ref=(g["grid"], g["refpsi"]))
+        for key in KEYS:
+            close(out[key], g[p + key], f"gpu psiref {p}{key}")
+        pl = gpu.BatchPlan(psiref_desc(N), B)
+        pl.set_policies(psiref_rows(g, B))
+        with pytest.raises(RuntimeError):      # psiref policies without a lane reference: refused
+            pl.solve(*_psiref_plan_inputs(g, p))
+        pl.set_lane_ref(g["grid"], g["refpsi"])
+        pl.solve(*_psiref_plan_inputs(g, p))
+        _psiref_tree_check(pl.tree(), g, p, B)

@@ -11,6 +11,7 @@ import pytest
 
 import hostsim_lib as H
 from common import golden, highway_desc_from_golden, highway_policy_rows
+from conftest import assert_solver_path
 
 pytestmark = pytest.mark.gpu
 
@@ -35,7 +36,7 @@ def _desc(g):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_robust_replay_gpu(gpu, name):
+def test_robust_replay_gpu(gpu, name, qp_path):
     """Every recorded step in one launch, each ego carrying the reference's warm start."""
     g = golden(name)
     T = len(g["traj_x"])
@@ -46,6 +47,7 @@ def test_robust_replay_gpu(gpu, name):
     warm = ~np.isnan(xl).any(axis=(1, 2))
     pl.set_robust_warm_start(np.nan_to_num(xl), np.nan_to_num(g["traj_ws_uLin"]), g["traj_ws_old"], mask=warm)
     r = pl.solve(g["traj_x"], g["traj_z"], g["traj_xRef"])
+    assert_solver_path(pl, qp_path)
     np.testing.assert_array_equal(r["status"], g["traj_status"])
     np.testing.assert_allclose(r["upred"], g["traj_uPred"], atol=1e-6)
     np.testing.assert_allclose(r["xpred"], g["traj_xPred"], atol=1e-6)

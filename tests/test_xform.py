@@ -153,15 +153,17 @@ def test_host_build_sticky_rows_matter():
 
 
 @pytest.mark.gpu
-def test_gpu_replays_xform_scene():
+def test_gpu_replays_xform_scene(solver_path):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from bmpc import plan
     g = golden(NAME)
     steps = len(g["traj_x"])
+    from conftest import assert_solver_path
     pl = plan.BatchPlan(xform_desc(g), 1)
     check_replay(replay(pl, g, steps), g, steps)
+    assert_solver_path(pl, solver_path)
 
 
 @pytest.mark.gpu

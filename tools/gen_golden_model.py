@@ -13,7 +13,7 @@ functions and evaluated through its public methods (``dyn_linearization``,
 ``branch_eval``, ``zpred_eval``, ``col_eval``; HMM: ``regressionAndLinearization``) on
 seeded points and on the inputs of the commented smoke test at
 ``quadruped_branch_dyn.py:250-272``.  Outputs: ``tests/golden/model_{highway,quadruped,
-hmm}.npz`` (inputs and outputs only).  Usage:  python tools/gen_golden_model.py
+hmm,merge,merge_psiref}.npz`` (inputs and outputs only).  Usage:  python tools/gen_golden_model.py
 """
 from __future__ import annotations
 
@@ -130,6 +130,65 @@ def gen_merge_model(H, utils, rng):
     return out
 
 
+def merge_reference_geometry():
+    """sim_merge's lane reference (main_branch.py:53-79): the reference's own merge_geometry
+    (Highway_env_branch.py:227-270) with N_lane 2, merge_lane 1, merge_s 50, merge_R 300."""
+    import importlib
+    try:
+        importlib.import_module("matplotlib")
+    except ImportError:   # plotting only; stubbed when absent
+        for mod in ("matplotlib", "matplotlib.pyplot", "matplotlib.patches", "matplotlib.animation"):
+            sys.modules.setdefault(mod, types.ModuleType(mod))
+        for sub in ("pyplot", "patches", "animation"):
+            setattr(sys.modules["matplotlib"], sub, sys.modules["matplotlib." + sub])
+    import Highway_env_branch as HE
+    assert os.path.dirname(os.path.abspath(HE.__file__)) == REF
+    X1, X2, Y1, Y2, psi1, psi2 = HE.merge_geometry(2, 1, 50, 300, 0)
+    return np.append(X1, X2), np.append(Y1, Y2), np.append(psi1, psi2), HE.v0
+
+
+def gen_merge_psiref(H, utils, rng):
+    """PredictiveModel_merge with the ramp's psiref-tracking backups -- sim_merge's pred_model[1]
+    (main_branch.py:82-85): [maintain_trackV(v0, refpsi), brake(refpsi)], refpsi the linear
+    interpolant of the ramp heading over the ramp's X grid (highway_branch_dyn.py:54-130,
+    400-502).  Points on, before and after the ramp grid and exactly on grid nodes."""
+    cons = utils.Branch_constants(s1=2, s2=3, c2=0.5, tran_diag=0.3, alpha=1, R=1.2, am=7.0, rm=0.3, J_c=20, s_c=1,
+                                  ylb=0., yub=7.2, L=4, W=2.5, col_alpha=5, Kpsi=0.1)
+    gX, gY, gpsi, v0 = merge_reference_geometry()
+    refY = H.interpolant('refY', 'linear', [gX], gY)
+    refpsi = H.interpolant('refpsi', 'linear', [gX], gpsi)
+    out = {"grid": gX, "refY": gY, "refpsi": gpsi, "v0": v0}
+    for ci, (N, K) in enumerate([(40, 14), (10, 8)]):
+        model = H.PredictiveModel_merge(4, 2, N, [lambda x: H.backup_maintain_trackV(x, cons, v0, refpsi),
+                                                  lambda x: H.backup_brake(x, cons, refpsi)], 0.1, cons,
+                                        (refY, refpsi), laneID=1, N_lane1=2, N_lane2=1)
+        X = rng.uniform(gX[0] - 10, gX[-1] + 10, K)
+        X[0], X[1], X[2] = gX[0] - 3.0, gX[-1] + 2.0, gX[len(gX) // 3]   # before / after the grid, on a node
+        y = np.interp(X, gX, gY) + rng.normal(0, 0.3, K)
+        psi = np.interp(X, gX, gpsi) + rng.normal(0, 0.02, K)
+        x = np.stack([X, y, rng.uniform(12, 24, K), psi], 1)
+        z = np.stack([X + rng.uniform(-15, 25, K), rng.choice([1.8, 5.4], K), rng.uniform(12, 24, K),
+                      rng.normal(0, 0.02, K)], 1)
+        z[3, 0:2] = x[3, 0:2]        # coincident positions: sign(0) = 0
+        u = np.stack([rng.uniform(-6, 6, K), rng.uniform(-0.3, 0.3, K)], 1)
+        rec = {k: [] for k in ("A", "B", "C", "xp", "p", "dp", "zpred", "h0", "dh")}
+        for k in range(K):
+            A, B, C, xp = model.dyn_linearization(x[k], u[k])
+            p, dp = model.branch_eval(x[k], z[k])
+            zp = model.zpred_eval(z[k])
+            h0, dh = model.col_eval(x[k], z[k])
+            for key, v in zip(rec, (A, B, C, xp, p, dp, zp, h0, dh)):
+                rec[key].append(np.asarray(v, float))
+        pre = f"c{ci}_"
+        out[pre + "N"] = N
+        out[pre + "x"], out[pre + "z"], out[pre + "u"] = x, z, u
+        for key, v in rec.items():
+            out[pre + key] = np.array(v)
+    out["ncases"] = 2
+    out["dt"], out["L"], out["W"], out["s1"], out["Kpsi"] = 0.1, 4.0, 2.5, 2.0, 0.1
+    return out
+
+
 def gen_quadruped(Q, utils, rng):
     out = {}
     # (N, dt, v0, L1, W1, L2, W2, col_tol, K): main_quadruped.py:15-30, then the smoke test
@@ -213,6 +272,8 @@ def main():
     np.savez_compressed(os.path.join(OUT, "model_quadruped.npz"), **gen_quadruped(Q, utils, rng))
     np.savez_compressed(os.path.join(OUT, "model_hmm.npz"), **gen_hmm(HM, utils, rng))
     np.savez_compressed(os.path.join(OUT, "model_merge.npz"), **gen_merge_model(H, utils, np.random.default_rng(77)))
+    np.savez_compressed(os.path.join(OUT, "model_merge_psiref.npz"),
+                        **gen_merge_psiref(H, utils, np.random.default_rng(78)))
     print("wrote", [f for f in os.listdir(OUT) if f.startswith("model_")])
 
 
