@@ -23,6 +23,10 @@
  *   bmpc_set_fx        <- solve(..., Fx) argument          MPC_branch.py:2055-2056
  *   bmpc_model_eval    <- PredictiveModel.dyn_linearization / branch_eval / zpred_eval /
  *                         col_eval                         highway_branch_dyn.py:284-325
+ *   bmpc_model_eval_ref<- the same of PredictiveModel_merge with psiref backups
+ *                                                          highway_branch_dyn.py:54-130,400-502
+ *   bmpc_set_lane_ref  <- PredictiveModel_merge(..., merge_ref) / the refpsi interpolant of
+ *                         the psiref backups              main_branch.py:78-85
  *   bmpc_env_step      <- Highway_env.step + Highway_sim collision rule
  *                                                          Highway_env_branch.py:83-184,421-429
  *
