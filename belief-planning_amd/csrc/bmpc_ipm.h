@@ -1412,19 +1412,22 @@ BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[N
   }
 }
 
-// Quads per task of a sweep with ntask tasks (1, 2 or 4; X::kChainQuads = 1 on the host): as
-// many as keep every task in one round of the executor's quads.  A task of G quads loads G
-// consecutive nodes per memory round trip (tree_solve, kkt_factor).
+// Quads per task of a sweep with ntask tasks over chains of len nodes (a power of two up to
+// X::kChainQuads, 1 on the host): as many as keep every task in one round of the executor's
+// quads (the wave's 16 or a multi-wave workgroup's) and no more than the chain has nodes.  A
+// task of G quads loads G consecutive nodes per memory round trip (tree_solve, kkt_factor).
 template <class X>
-BMPC_HD int chain_quads(const X& ex, int ntask) {
+BMPC_HD int chain_quads(const X& ex, int ntask, int len) {
   if constexpr (X::kChainQuads == 1) {
     (void)ex;
     (void)ntask;
+    (void)len;
     return 1;
   } else {
-    const int nq = ex.nlanes / X::kTaskLanes;
-    int G = X::kChainQuads;
-    while (G > 1 && ntask * G > nq) G >>= 1;
+    const int nq = (ex.nlanes < 64 ? ex.nlanes : 64) / X::kTaskLanes;   // a group stays in one wave
+    const int nqall = ex.nlanes / X::kTaskLanes;
+    int G = X::kChainQuads < nq ? X::kChainQuads : nq;
+    while (G > 1 && (ntask * G > nqall || G > len)) G >>= 1;
     return G;
   }
 }
@@ -1577,7 +1580,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
   // run the G node steps in turn, the cost-to-go rows Pn hopping to the next quad in between.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
-    const int G = chain_quads(ex, nbd);
+    const int G = chain_quads(ex, nbd, t.br_len[b0]);
     const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
     const int rounds = (nbd + slots - 1) / slots;
     for (int rd = 0; rd < rounds; ++rd) {
@@ -1658,7 +1661,8 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
         double Af[NX][NX], Bf[NX][NU];
         gather_rows(Ar, Af);
         gather_rows(Br, Bf);
-        for (int st = 0; st < G; ++st) {
+        const int nst = jb + 1 < G ? jb + 1 : G;
+        for (int st = 0; st < nst; ++st) {
           // every quad runs the step; quad st's operands are node jb - st and the carried Pn
           const bool mine = gq == st && has;
           double Pb[RX][NX];
@@ -1957,7 +1961,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       ncol += (c < 0 ? 0 : t.br_depth[c]) >= dep ? 1 : 0;
     }
     const int ntask = nfull + ncol;
-    const int G = chain_quads(ex, ntask);
+    const int G = chain_quads(ex, ntask, t.br_len[b0]);   // every branch of a depth has one length
     const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
     const int rounds = (ntask + slots - 1) / slots;
     const bool leaf = dep == P.NB;
@@ -2062,7 +2066,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
             }
           }
         }
-        for (int st = 0; st < G; ++st) {
+        const int nst = jb + 1 < G ? jb + 1 : G;   // the group's nodes (the last group may be short)
+        for (int st = 0; st < nst; ++st) {
           // every quad runs the step; quad st's operands are this group's node jb - st and the l
           // carried in from node jb - st + 1
           double g[RX], ln[RX], kfv[NU];
@@ -2102,7 +2107,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   for (int dep = 0; dep <= P.NB; ++dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
-    const int G = chain_quads(ex, ntask);   // quads per task (see the backward sweep)
+    const int G = chain_quads(ex, ntask, t.br_len[b0]);   // quads per task (see the backward sweep)
     const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
     const int rounds = (ntask + slots - 1) / slots;
     const bool leaf = dep == P.NB;
@@ -2141,7 +2146,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 #pragma unroll
         for (int m = 0; m < NU; ++m) kfu[m] = kfon ? kf[u * NU + m] : 0.0;
         const bool last = !(jc < len - 1 || leaf);   // the branch's last node feeds its children
-        for (int st = 0; st < G; ++st) {
+        const int nst = len - jb < G ? len - jb : G;
+        for (int st = 0; st < nst; ++st) {
           // every quad runs the step; quad st's operands are node jb + st and the carried state
           const bool mine = gq == st && has;
           // ---- u = kf + K x ----
@@ -2196,32 +2202,63 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   BMPC_TOC(C.ws, L, PROF_X3, t_fw);
   BMPC_TIC(t_post);
   // ---- post-pass: nu_k = -(l_k + P_k x_k), slack recovery -----------------------------------
-  for (int ri = 0; ri < nr; ++ri) {
-    gdouble* o = o0 + ri * os;
-    const gdouble* rr = r0 + ri * rs;
-    const gdouble* lvec = lv_ + ri * lstr;
+  // right-hand sides four per pass: a node's P row, dh and slack weights are loaded once for
+  // the four (the coupling solve's nc + 2 right-hand sides re-read them per rhs otherwise);
+  // every value is formed exactly as one rhs per pass forms it
+  constexpr int RB = 4;
+  struct VR { double v[RB]; };
+  for (int rb = 0; rb < nr; rb += RB) {
+    const int rn = nr - rb < RB ? nr - rb : RB;
     if (n0) {
-      gdouble* nn = n0 + ri * ns;
-      const bool lon = ex.uniform(ri >= ncw);   // Woodbury columns: l = 0 off the column's root path
       lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
-        double v = (lon || needed(t.x_branch[k], ri)) ? lvec[it] : 0.0;
+        double pr[NX];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) v += ws[L.P + k * NX * NX + i * NX + j] * o[P.oX + k * NX + j];
-        return -v;
-      }, [&](int it, double v) { nn[it] = v; });
+        for (int j = 0; j < NX; ++j) pr[j] = ws[L.P + k * NX * NX + i * NX + j];
+        VR out;
+#pragma unroll
+        for (int a2 = 0; a2 < RB; ++a2) {
+          const int ri = rb + (a2 < rn ? a2 : 0);
+          const gdouble* o = o0 + ri * os;
+          // Woodbury columns: l = 0 off the column's root path
+          double v = (ri >= ncw || needed(t.x_branch[k], ri)) ? lv_[ri * lstr + it] : 0.0;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) v += pr[j] * o[P.oX + k * NX + j];
+          out.v[a2] = -v;
+        }
+        return out;
+      }, [&](int it, const VR& r) {
+#pragma unroll
+        for (int a2 = 0; a2 < RB; ++a2)
+          if (a2 < rn) n0[(rb + a2) * ns + it] = r.v[a2];
+      });
     }
     lane_batch<BMPC_TS_UN>(ex, 0, P.T * Nc, [&](int it) {
       const int k = it / Nc, c = it % Nc;
       const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
-      double fx = 0.0;
+      double cf[NX];
 #pragma unroll
       for (int j = 0; j < NX; ++j) {   // -dh for c == 0, Fx[c-1] otherwise (blend: no branch around the dh load)
         const double dhv = dh[k * NX + j], fxj = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
-        fx += (m0 * (-dhv) + (1.0 - m0) * fxj) * o[P.oX + k * NX + j];
+        cf[j] = m0 * (-dhv) + (1.0 - m0) * fxj;
       }
-      return (rr[P.oS + it] + sdv[it * 2 + 1] * on * fx) / sdv[it * 2];
-    }, [&](int it, double v) { o[P.oS + it] = v; });
+      const double s1 = sdv[it * 2 + 1], s0 = sdv[it * 2];
+      VR out;
+#pragma unroll
+      for (int a2 = 0; a2 < RB; ++a2) {
+        const int ri = rb + (a2 < rn ? a2 : 0);
+        const gdouble* o = o0 + ri * os;
+        double fx = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) fx += cf[j] * o[P.oX + k * NX + j];
+        out.v[a2] = (r0[ri * rs + P.oS + it] + s1 * on * fx) / s0;
+      }
+      return out;
+    }, [&](int it, const VR& r) {
+#pragma unroll
+      for (int a2 = 0; a2 < RB; ++a2)
+        if (a2 < rn) o0[(rb + a2) * os + P.oS + it] = r.v[a2];
+    });
   }
   ex.sync();
   BMPC_TOC(C.ws, L, PROF_X4, t_post);
