@@ -120,11 +120,16 @@ struct DevExecT {
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
     return v;
   }
-  // K sums at once (in place)
+  // K sums / minima at once (in place)
   template <int K>
   __device__ void sum_n(double* v) const {
 #pragma unroll
     for (int k = 0; k < K; ++k) v[k] = sum(v[k]);
+  }
+  template <int K>
+  __device__ void min_n(double* v) const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = min(v[k]);
   }
 };
 
@@ -206,6 +211,8 @@ struct DevBlockExecT {
   __device__ double min(double v) const { reduce<2, 1>(&v); return v; }
   template <int K>
   __device__ void sum_n(double* v) const { reduce<0, K>(v); }
+  template <int K>
+  __device__ void min_n(double* v) const { reduce<2, K>(v); }
 };
 
 #if defined(BMPC_WITH_PHASED)

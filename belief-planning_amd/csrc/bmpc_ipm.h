@@ -1018,8 +1018,10 @@ BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam,
     one(d1, a1);
     one(d2, a2);
   }
-  const double a = fmin(ex.min(a1), ex.min(a2));
-  return ex.max(bad) > 0.0 ? 0.0 : a;
+  double mm[3] = {a1, a2, -bad};   // both minima and the max of bad in one reduction
+  ex.template min_n<3>(mm);
+  const double a = fmin(mm[0], mm[1]);
+  return -mm[2] > 0.0 ? 0.0 : a;
 }
 
 // out1 = W^-1 in and out2 = W^-1 out1 in one pass (kkt_solve: r3h and the G' operand of
@@ -2860,21 +2862,24 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     }, [&](int i, R5 r) { rz[i] = r.v; acz[0] += r.v * r.v; acz[1] += r.a; acz[2] += r.b; acz[3] += r.c; acz[4] += r.d; });
     ex.sync();
     const double cx = x[P.oJ];
-    const double by = ex.sum(acy[1]), hz = ex.sum(acz[1]);
+    // the ten sums in one reduction (one barrier pair on a multi-wave executor)
+    double rsum[10] = {acy[1], acz[1], acx[1], acy[2], acz[2], acz[3], acz[4], acy[0], acz[0], acx[0]};
+    ex.template sum_n<10>(rsum);
+    const double by = rsum[0], hz = rsum[1];
     const double rt = kap + cx + by + hz;
-    const double nx = sqrt(ex.sum(acx[1])), ny = sqrt(ex.sum(acy[2]));
-    const double nz = sqrt(ex.sum(acz[2])), ns = sqrt(ex.sum(acz[3]));
-    const double sz = ex.sum(acz[4]);
+    const double nx = sqrt(rsum[2]), ny = sqrt(rsum[3]);
+    const double nz = sqrt(rsum[4]), ns = sqrt(rsum[5]);
+    const double sz = rsum[6];
     const double mu = (sz + kap * tau) / (deg + 1.0);
     const double gap = sz / (tau * tau);
     const double pcost = cx / tau, dcost = -(hz + by) / tau;
     double relgap = -1.0;   // -1 = NaN
     if (pcost < 0.0) relgap = gap / (-pcost);
     else if (dcost > 0.0) relgap = gap / dcost;
-    const double nry = neq ? sqrt(ex.sum(acy[0])) / fmax(resy0 + nx, 1.0) : 0.0;
-    const double nrz = sqrt(ex.sum(acz[0])) / fmax(resz0 + nx + ns, 1.0);
+    const double nry = neq ? sqrt(rsum[7]) / fmax(resy0 + nx, 1.0) : 0.0;
+    const double nrz = sqrt(rsum[8]) / fmax(resz0 + nx + ns, 1.0);
     const double pres = fmax(nry, nrz) / tau;
-    const double dres = sqrt(ex.sum(acx[0])) / fmax(resx0 + ny + nz, 1.0) / tau;
+    const double dres = sqrt(rsum[9]) / fmax(resx0 + ny + nz, 1.0) / tau;
     BMPC_TOC(ws, L, PROF_RESID, t_res);
     // infeasibility certificates (only evaluated when their preconditions hold)
     double pinfres = -1.0, dinfres = -1.0;

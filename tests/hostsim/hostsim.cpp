@@ -53,6 +53,8 @@ struct HostExecT {
   double min(double v) const { return v; }
   template <int K>
   void sum_n(double*) const {}
+  template <int K>
+  void min_n(double*) const {}
 };
 using HostExec = HostExecT<false>;
 
