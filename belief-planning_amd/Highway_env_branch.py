@@ -67,9 +67,20 @@ class Highway_env:
     def step(self, t_):
         n = self.predictiveModel.n
         xx_set = [None] * self.NV
+        # the vehicles' backup rollouts in batched calls (one bmpc_model_eval launch each): vehicles
+        # 0 and 1 together -- update_backup below runs at i == 1 only, after that vehicle's
+        # rollout -- and the rest after it, as the reference's per-vehicle loop sees the policies
+        states = [np.asarray(v.state, float) for v in self.veh_set]
+        head = self.predictiveModel.zpred_eval(np.stack(states[:2]))
+        tail = None
         for i, veh in enumerate(self.veh_set):
             z = veh.state
-            xx_set[i] = self.predictiveModel.zpred_eval(z)
+            if i < 2:
+                xx_set[i] = head[i]
+            else:
+                if tail is None:
+                    tail = self.predictiveModel.zpred_eval(np.stack(states[2:]))
+                xx_set[i] = tail[i - 2]
             new = round((z[1] - 1.8) / 3.6)
             if t_ == 0 or (new != veh.laneidx and abs(z[1] - 1.8 - 3.6 * new) < 1.4):
                 veh.laneidx = new
@@ -211,7 +222,12 @@ class Highway_env_merge:
         for i, veh in enumerate(self.veh_set):
             if veh.state[0] > self.merge_s + 8:
                 self.laneID[i] = 0
-            xx_set[i] = self.pred_model[self.laneID[i]].zpred_eval(veh.state)
+        # one batched rollout call per lane model (the ramp's psiref model runs on the GPU too)
+        for lid in sorted(set(self.laneID)):
+            idx = [i for i in range(self.NV) if self.laneID[i] == lid]
+            zz = self.pred_model[lid].zpred_eval(np.stack([np.asarray(self.veh_set[i].state, float) for i in idx]))
+            for j, i in enumerate(idx):
+                xx_set[i] = zz[j]
         for i, veh in enumerate(self.veh_set):
             veh.backupidx = 0
             u0_set[i] = self.backupcons[self.laneID[i]][0](veh.state)

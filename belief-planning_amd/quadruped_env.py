@@ -80,7 +80,8 @@ class Quad_env:
     def step(self, t_):
         n = self.predictiveModel.n
         u_set, x_set, u0_set = [None] * self.NR, [None] * self.NR, [None] * self.NR
-        xx_set = [self.predictiveModel.zpred_eval(r.state) for r in self.robot_set]
+        zz = self.predictiveModel.zpred_eval(np.stack([np.asarray(r.state, float) for r in self.robot_set]))
+        xx_set = [zz[i] for i in range(self.NR)]   # every robot's rollouts in one batched call
         idx0 = self.robot_set[0].backupidx
         x1 = xx_set[0][:, idx0 * n:(idx0 + 1) * n]
         ego = self.robot_set[0]
