@@ -3,6 +3,7 @@
 # argument (a space-separated counter list, within the per-block limits of
 # MI355X_MICROARCH.md), each its own run; per-dispatch averages of the IPM kernel, cold first
 # solve dropped.  usage: bash tools/pmc_probe.sh TAG "C1 C2" "C3" ...
+# (QB_ARGS: quick_bench arguments "B N NB", default 4096; KF: kernel-name regex, default k_ipm|k_solve)
 tag=$1; shift
 R=$PWD
 out=$R/gpurun_out/$tag
@@ -15,13 +16,13 @@ for cs in "$@"; do
     -- python3 $R/tools/quick_bench.py ${QB_ARGS:-4096} > $out/p$i.log 2>&1
   echo "pass $i ($cs): rc $?" >> $out/summary.txt
 done
-python3 - $out >> $out/summary.txt <<'PY'
-import csv, glob, sys, collections
-out = sys.argv[1]
+python3 - $out "${KF:-k_ipm|k_solve}" >> $out/summary.txt <<'PY'
+import csv, glob, re, sys, collections
+out, kf = sys.argv[1], re.compile(sys.argv[2])
 per = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_ipm" in r["Kernel_Name"] or "k_solve" in r["Kernel_Name"]:
+        if kf.search(r["Kernel_Name"]):
             per[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
 for c, d in sorted(per.items()):
     vals = [v for _, v in sorted(d.items())][1:] or list(d.values())

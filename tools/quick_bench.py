@@ -1,4 +1,5 @@
-"""Quick GPU timing of one batched solve (development helper)."""
+"""Quick GPU timing of one batched solve (development helper).
+    python tools/quick_bench.py [B] [N] [NB]     (QB_TRANSFORM=1: a BMPC_PLAN_TRANSFORM plan)"""
 import os
 import sys
 import time
@@ -14,7 +15,11 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 NB = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 x, z, xref, tgt = seeded_batch(B, 0)
-pl = plan.BatchPlan(highway_desc(N, NB), B)
+desc = highway_desc(N, NB)
+if os.environ.get("QB_TRANSFORM"):   # the drop-in BranchMPC_CVaR's plan (per-ego S / Fx / bx path)
+    from bmpc import abi
+    desc.flags |= abi.PLAN_TRANSFORM
+pl = plan.BatchPlan(desc, B)
 pl.set_policies(highway_policy_rows(tgt))
 pl.enable_timing(True)
 for step in range(4):
