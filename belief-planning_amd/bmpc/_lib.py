@@ -128,12 +128,19 @@ _SIGS = {
 EXPORTED = tuple(_SIGS)
 
 
-def load(path: str = SO_PATH):
-    """Load a libbmpc.so and declare the C ABI (no device access)."""
+def load(path: str = SO_PATH, strict: bool = True):
+    """Load a libbmpc.so and declare the C ABI (no device access).  strict=False (another
+    build named by BMPC_LIBRARY, e.g. an older source for an A/B) tolerates entry points the
+    build lacks: calling one raises BmpcUnavailable."""
     if not os.path.exists(path):
         raise BmpcUnavailable(f"{path} not built; run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(path)
     for name, (res, args) in _SIGS.items():
+        if not strict and not hasattr(lib, name):
+            def missing(*a, _n=name):
+                raise BmpcUnavailable(f"{path} has no {_n}")
+            setattr(lib, name, missing)
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
@@ -145,7 +152,8 @@ def lib():
     sources (e.g. libbmpc_prof.so for phase counters)."""
     global _LIB
     if _LIB is None:
-        _LIB = load(os.environ.get("BMPC_LIBRARY", SO_PATH))
+        path = os.environ.get("BMPC_LIBRARY", SO_PATH)
+        _LIB = load(path, strict=os.path.abspath(path) == os.path.abspath(SO_PATH))
     return _LIB
 
 

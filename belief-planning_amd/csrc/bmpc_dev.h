@@ -34,24 +34,6 @@ __device__ __forceinline__ double dpp_d(double v) {
   return __hiloint2double(hi, lo);
 }
 
-// The value of the previous quad of a chain group of G quads (1, 2, 4, 8 or 16, aligned in the
-// wave), cyclically: quad gq receives quad (gq - 1) mod G.  Inside a DPP row of 16 lanes
-// (G <= 4) row_ror:4 moves every quad's value to the next quad of its row, and in groups of two
-// the first quad takes its partner's value by row_ror:12 instead; wider groups span rows and
-// go through ds_bpermute.
-__device__ __forceinline__ double chain_prev(double v, int G, int gq) {
-  if (G == 1) return v;
-  if (G > 4) {
-    const int lane = __lane_id();
-    const int span = 4 * G, base = lane & ~(span - 1);
-    return __shfl(v, base + ((lane - base - 4) & (span - 1)), 64);
-  }
-  const double r4 = dpp_d<0x124>(v);    // row_ror:4
-  if (G == 4) return r4;
-  const double r12 = dpp_d<0x12C>(v);   // row_ror:12
-  return gq == 0 ? r12 : r4;
-}
-
 template <bool TR, bool TL = true>
 struct DevExecT {
   static constexpr bool kTransform = TR;   // per-ego S / bx constants in LDS (merge plans)
@@ -75,10 +57,6 @@ struct DevExecT {
   }
   // task groups of 4 lanes (one DPP quad) for the tree sweeps
   static constexpr int kTaskLanes = 4;
-  // a sweep task may span up to 16 quads (bmpc_ipm.h, chain_quads): the quads load consecutive
-  // nodes together and the recursion hops from quad to quad
-  static constexpr int kChainQuads = 16;
-  __device__ double qprev(double v, int G, int gq) const { return chain_prev(v, G, gq); }
   // cone rows per lane the fused IPM passes hold in registers (bmpc_ipm.h, cone_regs)
   static constexpr int kConeRegRows = 8;
   __device__ double tsum(double v) const {
@@ -153,8 +131,6 @@ struct DevBlockExecT {
   static constexpr int nlanes = 64 * NW;
   static constexpr bool kRowLanes = true;
   static constexpr int kTaskLanes = 4;
-  static constexpr int kChainQuads = 16;
-  __device__ double qprev(double v, int G, int gq) const { return chain_prev(v, G, gq); }
   static constexpr int kConeRegRows = 8;
   static constexpr int kRedMax = 16;
   __device__ double tsum(double v) const {

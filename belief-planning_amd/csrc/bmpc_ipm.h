@@ -1414,26 +1414,6 @@ BMPC_HD void task_gather(const X& ex, const double (&mine)[RX], double (&full)[N
   }
 }
 
-// Quads per task of a sweep with ntask tasks over chains of len nodes (a power of two up to
-// X::kChainQuads, 1 on the host): as many as keep every task in one round of the executor's
-// quads (the wave's 16 or a multi-wave workgroup's) and no more than the chain has nodes.  A
-// task of G quads loads G consecutive nodes per memory round trip (tree_solve, kkt_factor).
-template <class X>
-BMPC_HD int chain_quads(const X& ex, int ntask, int len) {
-  if constexpr (X::kChainQuads == 1) {
-    (void)ex;
-    (void)ntask;
-    (void)len;
-    return 1;
-  } else {
-    const int nq = (ex.nlanes < 64 ? ex.nlanes : 64) / X::kTaskLanes;   // a group stays in one wave
-    const int nqall = ex.nlanes / X::kTaskLanes;
-    int G = X::kChainQuads < nq ? X::kChainQuads : nq;
-    while (G > 1 && (ntask * G > nqall || G > len)) G >>= 1;
-    return G;
-  }
-}
-
 // ------------------------------------------------------------------------------------
 // KKT factorisation
 // ------------------------------------------------------------------------------------
@@ -1578,41 +1558,29 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
   // Lane-varying picks (row gi's column of a matrix every lane holds) are taken while the
   // values are formed, as selects between fresh values: a select chain over a register array's
   // elements would be folded into a runtime index, i.e. the array moved to scratch memory.
-  // A branch spans G quads (chain_quads): they load G consecutive nodes in one round trip and
-  // run the G node steps in turn, the cost-to-go rows Pn hopping to the next quad in between.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
-    const int G = chain_quads(ex, nbd, t.br_len[b0]);
-    const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
-    const int rounds = (nbd + slots - 1) / slots;
+    const int rounds = (nbd + ngrp - 1) / ngrp;
     for (int rd = 0; rd < rounds; ++rd) {
-      const int bi = rd * slots + tslot;
+      const int bi = rd * ngrp + grp;
       if (bi >= nbd) continue;   // whole group idle together
       const int b = b0 + bi;
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const bool leaf = dep == P.NB;
       double Pn[RX][NX];   // this lane's rows of the cost-to-go after the current node
-#pragma unroll
-      for (int q = 0; q < RX; ++q)
-#pragma unroll
-        for (int j = 0; j < NX; ++j) Pn[q][j] = 0.0;
-      if (leaf) {   // terminal node: P = hx (every quad of the branch holds it)
+      if (leaf) {   // terminal node: P = hx
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
 #pragma unroll
           for (int j = 0; j < NX; ++j) Pn[q][j] = ws[L.hx + (ndx + len) * NX * NX + i * NX + j];
-          if (gl * RX + q < NX && gq == 0)
+          if (gl * RX + q < NX)
 #pragma unroll
             for (int j = 0; j < NX; ++j) ws[L.P + (ndx + len) * NX * NX + i * NX + j] = Pn[q][j];
         }
       }
-      for (int jb = len - 1; jb >= 0; jb -= G) {
-        const int jn = jb - gq;               // this quad's node
-        const bool has = jn >= 0;
-        const int jc = has ? jn : 0;
-        const int k = ndx + jc, u = ndu + jc;
-        const bool first = !(jc < len - 1 || leaf);   // the children's P rows replace the carried Pn
+      for (int jn = len - 1; jn >= 0; --jn) {
+        const int k = ndx + jn, u = ndu + jn;
         // this lane's rows of the node's data (independent of the recursion)
         double Hx[RX][NX], Ar[RX][NX], Ac[RX][NX], Br[RX][NU], Hu[NU][NU];
 #pragma unroll
@@ -1628,14 +1596,19 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
           for (int m = 0; m < NU; ++m) Br[q][m] = Bd[u * NX * NU + i * NU + m];
         }
         mat_load(Hu, ws + L.hu + u * NU * NU);
-        double Pch[RX][NX];
+        double Pb[RX][NX];
+        if (jn < len - 1 || leaf) {
 #pragma unroll
-        for (int q = 0; q < RX; ++q)
+          for (int q = 0; q < RX; ++q)
 #pragma unroll
-          for (int c = 0; c < NX; ++c) Pch[q][c] = 0.0;
-        if (first) {
+            for (int c = 0; c < NX; ++c) Pb[q][c] = Pn[q][c];
+        } else {
           // the children's first-node P rows (written by the previous depth phase), in the
           // order riccati_step's caller sums them (pairs, the odd one padded with weight 0)
+#pragma unroll
+          for (int q = 0; q < RX; ++q)
+#pragma unroll
+            for (int c = 0; c < NX; ++c) Pb[q][c] = 0.0;
           const int c0 = t.br_child0[b];
           for (int i0 = 0; i0 < P.m; i0 += 2) {
             double Pc[2][RX][NX];
@@ -1655,7 +1628,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
 #pragma unroll
               for (int q = 0; q < RX; ++q)
 #pragma unroll
-                for (int c = 0; c < NX; ++c) Pch[q][c] += w * Pc[h][q][c];
+                for (int c = 0; c < NX; ++c) Pb[q][c] += w * Pc[h][q][c];
             }
           }
         }
@@ -1663,149 +1636,132 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
         double Af[NX][NX], Bf[NX][NU];
         gather_rows(Ar, Af);
         gather_rows(Br, Bf);
-        const int nst = jb + 1 < G ? jb + 1 : G;
-        for (int st = 0; st < nst; ++st) {
-          // every quad runs the step; quad st's operands are node jb - st and the carried Pn
-          const bool mine = gq == st && has;
-          double Pb[RX][NX];
+        // M = Pb A (own rows), then the full M
+        double Mr[RX][NX], Mf[NX][NX];
 #pragma unroll
-          for (int q = 0; q < RX; ++q)
-#pragma unroll
-            for (int c = 0; c < NX; ++c) Pb[q][c] = first ? Pch[q][c] : Pn[q][c];
-          // M = Pb A (own rows), then the full M
-          double Mr[RX][NX], Mf[NX][NX];
-#pragma unroll
-          for (int q = 0; q < RX; ++q)
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-              double v = 0.0;
-#pragma unroll
-              for (int r = 0; r < NX; ++r) v += Pb[q][r] * Af[r][j];
-              Mr[q][j] = v;
-            }
-          gather_rows(Mr, Mf);
-          // Pk = Hx + A'M (own rows)
-          double Pk[RX][NX];
-#pragma unroll
-          for (int q = 0; q < RX; ++q)
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-              double v = 0.0;
-#pragma unroll
-              for (int r = 0; r < NX; ++r) v += Ac[q][r] * Mf[r][j];
-              Pk[q][j] = Hx[q][j] + v;
-            }
-          // Qux = B'M and Quu = Hu + B'(Pb B) (full, every lane)
-          double Qux[NU][NX], Quu[NU][NU], qc[RX][NU];   // qc: column gl*RX+q of Qux
-#pragma unroll
-          for (int i = 0; i < NU; ++i)
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-              double v = 0.0;
-#pragma unroll
-              for (int r = 0; r < NX; ++r) v += Bf[r][i] * Mf[r][j];
-              Qux[i][j] = v;
-#pragma unroll
-              for (int q = 0; q < RX; ++q) qc[q][i] = (j == gl * RX + q || j == 0) ? v : qc[q][i];
-            }
-          double PBr[RX][NU], PBf[NX][NU];   // Pb B
-#pragma unroll
-          for (int q = 0; q < RX; ++q)
-#pragma unroll
-            for (int j = 0; j < NU; ++j) {
-              double pb = 0.0;
-#pragma unroll
-              for (int c = 0; c < NX; ++c) pb += Pb[q][c] * Bf[c][j];
-              PBr[q][j] = pb;
-            }
-          gather_rows(PBr, PBf);
-          mat_copy(Hu, Quu);
-#pragma unroll
-          for (int i = 0; i < NU; ++i)
-#pragma unroll
-            for (int j = 0; j < NU; ++j) {
-              double v = 0.0;
-#pragma unroll
-              for (int r = 0; r < NX; ++r) v += Bf[r][i] * PBf[r][j];
-              Quu[i][j] += v;
-            }
-          if (!chol<NU>(Quu) && mine) bad = 1.0;
-          double Qi[NU][NU];   // Quu^-1 (the tree sweeps multiply by it)
-#pragma unroll
-          for (int j = 0; j < NU; ++j) {
-            double col[NU];
-#pragma unroll
-            for (int i = 0; i < NU; ++i) col[i] = i == j ? 1.0 : 0.0;
-            chol_solve<NU>(Quu, col);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) Qi[i][j] = col[i];
-          }
-          double K[NU][NX], kc[RX][NU];   // kc: column gl*RX+q of K
+        for (int q = 0; q < RX; ++q)
 #pragma unroll
           for (int j = 0; j < NX; ++j) {
-            double col[NU];
+            double v = 0.0;
 #pragma unroll
-            for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
-            chol_solve<NU>(Quu, col);
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-              K[i][j] = col[i];
-#pragma unroll
-              for (int q = 0; q < RX; ++q) kc[q][i] = (j == gl * RX + q || j == 0) ? col[i] : kc[q][i];
-            }
+            for (int r = 0; r < NX; ++r) v += Pb[q][r] * Af[r][j];
+            Mr[q][j] = v;
           }
-          // Pk += Qux' K (own rows), then symmetrise: P[i][j] = P[j][i] = (P[lo][hi] + P[hi][lo]) / 2
+        gather_rows(Mr, Mf);
+        // Pk = Hx + A'M (own rows)
+        double Pk[RX][NX];
 #pragma unroll
-          for (int q = 0; q < RX; ++q)
+        for (int q = 0; q < RX; ++q)
 #pragma unroll
-            for (int j = 0; j < NX; ++j) {
-              double v = 0.0;
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
 #pragma unroll
-              for (int r = 0; r < NU; ++r) v += qc[q][r] * K[r][j];
-              Pk[q][j] += v;
-            }
-          // column gl*RX+q of the full Pk, gathered column by column
-          double pcol[RX][NX];
-#pragma unroll
-          for (int c = 0; c < NX; ++c) {
-            double cm[RX], fc[NX];
-#pragma unroll
-            for (int q = 0; q < RX; ++q) cm[q] = Pk[q][c];
-            task_gather<NX, RX, W>(ex, cm, fc);
-#pragma unroll
-            for (int q = 0; q < RX; ++q)
-#pragma unroll
-              for (int r = 0; r < NX; ++r) pcol[q][r] = (c == gl * RX + q || c == 0) ? fc[r] : pcol[q][r];
+            for (int r = 0; r < NX; ++r) v += Ac[q][r] * Mf[r][j];
+            Pk[q][j] = Hx[q][j] + v;
           }
-          double Pnew[RX][NX];
+        // Qux = B'M and Quu = Hu + B'(Pb B) (full, every lane)
+        double Qux[NU][NX], Quu[NU][NU], qc[RX][NU];   // qc: column gl*RX+q of Qux
 #pragma unroll
-          for (int q = 0; q < RX; ++q) {
-            const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+        for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int j = 0; j < NX; ++j) {
-              const double pij = Pk[q][j], pji = pcol[q][j];   // own row entry, column entry
-              Pnew[q][j] = i == j ? pij : i < j ? 0.5 * (pij + pji) : 0.5 * (pji + pij);
-            }
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Bf[r][i] * Mf[r][j];
+            Qux[i][j] = v;
+#pragma unroll
+            for (int q = 0; q < RX; ++q) qc[q][i] = (j == gl * RX + q || j == 0) ? v : qc[q][i];
           }
-          // stores: P rows, K columns (lane gl: entries j = gl*RX + q), Quu^-1 (lane gl 0)
-          if (mine) {
+        double PBr[RX][NU], PBf[NX][NU];   // Pb B
 #pragma unroll
-            for (int q = 0; q < RX; ++q) {
-              const int i = gl * RX + q;
-              if (i < NX) {
+        for (int q = 0; q < RX; ++q)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) ws[L.P + k * NX * NX + i * NX + j] = Pnew[q][j];
+          for (int j = 0; j < NU; ++j) {
+            double pb = 0.0;
 #pragma unroll
-                for (int m = 0; m < NU; ++m) ws[L.Kg + u * NU * NX + m * NX + i] = kc[q][m];
-              }
-            }
-            if (gl == 0) mat_store(Qi, ws + L.Luu + u * NU * NU);
+            for (int c = 0; c < NX; ++c) pb += Pb[q][c] * Bf[c][j];
+            PBr[q][j] = pb;
           }
+        gather_rows(PBr, PBf);
+        mat_copy(Hu, Quu);
 #pragma unroll
-          for (int q = 0; q < RX; ++q)
+        for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int j = 0; j < NX; ++j) Pn[q][j] = ex.qprev(Pnew[q][j], G, gq);
+          for (int j = 0; j < NU; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) v += Bf[r][i] * PBf[r][j];
+            Quu[i][j] += v;
+          }
+        if (!chol<NU>(Quu)) bad = 1.0;
+        double Qi[NU][NU];   // Quu^-1 (the tree sweeps multiply by it)
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+          double col[NU];
+#pragma unroll
+          for (int i = 0; i < NU; ++i) col[i] = i == j ? 1.0 : 0.0;
+          chol_solve<NU>(Quu, col);
+#pragma unroll
+          for (int i = 0; i < NU; ++i) Qi[i][j] = col[i];
         }
+        double K[NU][NX], kc[RX][NU];   // kc: column gl*RX+q of K
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          double col[NU];
+#pragma unroll
+          for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
+          chol_solve<NU>(Quu, col);
+#pragma unroll
+          for (int i = 0; i < NU; ++i) {
+            K[i][j] = col[i];
+#pragma unroll
+            for (int q = 0; q < RX; ++q) kc[q][i] = (j == gl * RX + q || j == 0) ? col[i] : kc[q][i];
+          }
+        }
+        // Pk += Qux' K (own rows), then symmetrise: P[i][j] = P[j][i] = (P[lo][hi] + P[hi][lo]) / 2
+#pragma unroll
+        for (int q = 0; q < RX; ++q)
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < NU; ++r) v += qc[q][r] * K[r][j];
+            Pk[q][j] += v;
+          }
+        // column gl*RX+q of the full Pk, gathered column by column
+        double pcol[RX][NX];
+#pragma unroll
+        for (int c = 0; c < NX; ++c) {
+          double cm[RX], fc[NX];
+#pragma unroll
+          for (int q = 0; q < RX; ++q) cm[q] = Pk[q][c];
+          task_gather<NX, RX, W>(ex, cm, fc);
+#pragma unroll
+          for (int q = 0; q < RX; ++q)
+#pragma unroll
+            for (int r = 0; r < NX; ++r) pcol[q][r] = (c == gl * RX + q || c == 0) ? fc[r] : pcol[q][r];
+        }
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            const double pij = Pk[q][j], pji = pcol[q][j];   // own row entry, column entry
+            Pn[q][j] = i == j ? pij : i < j ? 0.5 * (pij + pji) : 0.5 * (pji + pij);
+          }
+        }
+        // stores: P rows, K columns (lane gl: entries j = gl*RX + q), Quu^-1 (lane gl 0)
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q;
+          if (i < NX) {
+#pragma unroll
+            for (int j = 0; j < NX; ++j) ws[L.P + k * NX * NX + i * NX + j] = Pn[q][j];
+#pragma unroll
+            for (int m = 0; m < NU; ++m) ws[L.Kg + u * NU * NX + m * NX + i] = kc[q][m];
+          }
+        }
+        if (gl == 0) mat_store(Qi, ws + L.Luu + u * NU * NU);
       }
     }
     ex.sync();
@@ -1948,10 +1904,7 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
 
   BMPC_TIC(t_bw);
   // ---- backward sweep (leaves -> root) -------------------------------------------------------
-  // The per-node loads do not depend on the recursion.  A task spans G quads (chain_quads):
-  // they load G consecutive nodes in one memory round trip, then run the G node steps in turn,
-  // the carried l hopping to the next quad between steps (chain_prev) -- the same operations
-  // on each node as one quad per task, G times fewer dependent round trips.
+  // The per-node loads do not depend on the recursion: one memory round trip per node.
   for (int dep = P.NB; dep >= 0; --dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     // the needed tasks of this depth, in order: first the (branch, rhs >= ncw) pairs, then for
@@ -1963,13 +1916,11 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       ncol += (c < 0 ? 0 : t.br_depth[c]) >= dep ? 1 : 0;
     }
     const int ntask = nfull + ncol;
-    const int G = chain_quads(ex, ntask, t.br_len[b0]);   // every branch of a depth has one length
-    const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
-    const int rounds = (ntask + slots - 1) / slots;
+    const int rounds = (ntask + ngrp - 1) / ngrp;
     const bool leaf = dep == P.NB;
     for (int rd = 0; rd < rounds; ++rd) {
-      const int task = rd * slots + tslot;
-      if (task >= ntask) continue;       // whole task group idle together
+      const int task = rd * ngrp + grp;
+      if (task >= ntask) continue;       // whole group idle together
       int b, ri;
       if (task < nfull) {
         b = b0 + task / (nr - ncw);
@@ -2000,25 +1951,18 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       const int ndx = t.br_ndx[b], ndu = t.br_ndu[b], len = t.br_len[b];
       const int c0 = t.br_child0[b];
       double l[RX];
-#pragma unroll
-      for (int q = 0; q < RX; ++q) l[q] = 0.0;   // (a non-leaf branch's first step takes no l)
-      if (leaf) {   // terminal node: l = -r_x (= qx0 there); every quad of the task holds it
+      if (leaf) {   // terminal node: l = -r_x (= qx0 there)
         const int tn = ndx + len;
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q;
           l[q] = i < NX ? (pre ? q0[tn * NX + i] : qx0(rr, tn, i)) : 0.0;
-          if (i < NX && gq == 0) lvec[tn * NX + i] = l[q];
+          if (i < NX) lvec[tn * NX + i] = l[q];
         }
       }
-      for (int jb = len - 1; jb >= 0; jb -= G) {
-        // this quad's node (jb - gq) and everything its step reads but the carried l
-        const int jn = jb - gq;
-        const bool has = jn >= 0;
-        const int jc = has ? jn : 0;
-        const int k = ndx + jc, u = ndu + jc;
-        const bool first = jc == len - 1 && !leaf;   // children terms, no carried l
-        double qx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU], pe[RX], Pr[RX][NX], ec[NX];
+      for (int jn = len - 1; jn >= 0; --jn) {
+        const int k = ndx + jn, u = ndu + jn;
+        double qx[RX], Acol[RX][NX], Brow[RX][NU], Kcol[RX][NU], Lu[NU][NU], ru[NU];
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
@@ -2033,25 +1977,22 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         mat_load(Lu, ws + L.Luu + u * NU * NU);
 #pragma unroll
         for (int m = 0; m < NU; ++m) ru[m] = rr[P.oU + u * NU + m];
-        if (!first) {   // g = l + P_{k+1} e_{k+1}: P's rows and e, summed after l at the step
+        double g[RX];
+        if (jn < len - 1 || leaf) {
+          double ec[NX];
 #pragma unroll
           for (int j = 0; j < NX; ++j) ec[j] = ee[(k + 1) * NX + j];
 #pragma unroll
           for (int q = 0; q < RX; ++q) {
             const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
+            double v = l[q];
 #pragma unroll
-            for (int j = 0; j < NX; ++j) Pr[q][j] = ws[L.P + (k + 1) * NX * NX + i * NX + j];
-            pe[q] = 0.0;
+            for (int j = 0; j < NX; ++j) v += ws[L.P + (k + 1) * NX * NX + i * NX + j] * ec[j];
+            g[q] = v;
           }
-        } else {        // the children's l + P e (written by the previous depth)
+        } else {
 #pragma unroll
-          for (int j = 0; j < NX; ++j) ec[j] = 0.0;
-#pragma unroll
-          for (int q = 0; q < RX; ++q)
-#pragma unroll
-            for (int j = 0; j < NX; ++j) Pr[q][j] = 0.0;
-#pragma unroll
-          for (int q = 0; q < RX; ++q) pe[q] = 0.0;
+          for (int q = 0; q < RX; ++q) g[q] = 0.0;
           for (int ci = 0; ci < P.m; ++ci) {
             if (!needed(c0 + ci, ri)) continue;   // l = 0 and e = 0 there: adds exactly 0
             const int c = t.br_ndx[c0 + ci];
@@ -2064,36 +2005,20 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
               double v = lvec[c * NX + i];
 #pragma unroll
               for (int j = 0; j < NX; ++j) v += ws[L.P + c * NX * NX + i * NX + j] * ec[j];
-              pe[q] += v;
+              g[q] += v;
             }
           }
         }
-        const int nst = jb + 1 < G ? jb + 1 : G;   // the group's nodes (the last group may be short)
-        for (int st = 0; st < nst; ++st) {
-          // every quad runs the step; quad st's operands are this group's node jb - st and the l
-          // carried in from node jb - st + 1
-          double g[RX], ln[RX], kfv[NU];
+        double kfv[NU];
+        bw_node<X, NX, NU, RX, W>(ex, gl, qx, Acol, Brow, Kcol, Lu, ru, g, l, kfv);
 #pragma unroll
-          for (int q = 0; q < RX; ++q) {
-            double v = l[q];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) v += Pr[q][j] * ec[j];
-            g[q] = first ? pe[q] : v;
-          }
-          bw_node<X, NX, NU, RX, W>(ex, gl, qx, Acol, Brow, Kcol, Lu, ru, g, ln, kfv);
-          if (gq == st && has) {
-#pragma unroll
-            for (int q = 0; q < RX; ++q) {
-              const int i = gl * RX + q;
-              if (i < NX) lvec[k * NX + i] = ln[q];
-            }
-            if (gl == 0)
-#pragma unroll
-              for (int m = 0; m < NU; ++m) kf[u * NU + m] = kfv[m];
-          }
-#pragma unroll
-          for (int q = 0; q < RX; ++q) l[q] = ex.qprev(ln[q], G, gq);
+        for (int q = 0; q < RX; ++q) {
+          const int i = gl * RX + q;
+          if (i < NX) lvec[k * NX + i] = l[q];
         }
+        if (gl == 0)
+#pragma unroll
+          for (int m = 0; m < NU; ++m) kf[u * NU + m] = kfv[m];
       }
     }
     ex.sync();
@@ -2109,12 +2034,10 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   for (int dep = 0; dep <= P.NB; ++dep) {
     const int b0 = branch_start(P, dep), nbd = branch_count(P, dep);
     const int ntask = nbd * nr;
-    const int G = chain_quads(ex, ntask, t.br_len[b0]);   // quads per task (see the backward sweep)
-    const int slots = ngrp / G, tslot = grp / G, gq = grp % G;
-    const int rounds = (ntask + slots - 1) / slots;
+    const int rounds = (ntask + ngrp - 1) / ngrp;
     const bool leaf = dep == P.NB;
     for (int rd = 0; rd < rounds; ++rd) {
-      const int task = rd * slots + tslot;
+      const int task = rd * ngrp + grp;
       if (task >= ntask) continue;
       const int b = b0 + task / nr, ri = task % nr;
       gdouble* o = o0 + ri * os;
@@ -2126,14 +2049,11 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
       double xk[NX];      // full state (every lane of the group holds all of it)
 #pragma unroll
       for (int j = 0; j < NX; ++j) xk[j] = o[P.oX + ndx * NX + j];   // written by the parent group
-      for (int jb = 0; jb < len; jb += G) {
-        const int jn = jb + gq;                 // this quad's node
-        const bool has = jn < len;
-        const int jc = has ? jn : len - 1;
-        const int k = ndx + jc, u = ndu + jc;
+      for (int jn = 0; jn < len; ++jn) {
+        const int k = ndx + jn, u = ndu + jn;
         // ---- loads ----
         double Arow[RX][NX], Brow[RX][NU], Kcol[RX][NU], kfu[NU], en[RX];
-        const int kn = (jc < len - 1 || leaf) ? k + 1 : t.br_ndx[c0 >= 0 ? c0 : 0];
+        const int kn = (jn < len - 1 || leaf) ? k + 1 : t.br_ndx[c0 >= 0 ? c0 : 0];
 #pragma unroll
         for (int q = 0; q < RX; ++q) {
           const int i = gl * RX + q < NX ? gl * RX + q : NX - 1;
@@ -2147,55 +2067,46 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
         }
 #pragma unroll
         for (int m = 0; m < NU; ++m) kfu[m] = kfon ? kf[u * NU + m] : 0.0;
-        const bool last = !(jc < len - 1 || leaf);   // the branch's last node feeds its children
-        const int nst = len - jb < G ? len - jb : G;
-        for (int st = 0; st < nst; ++st) {
-          // every quad runs the step; quad st's operands are node jb + st and the carried state
-          const bool mine = gq == st && has;
-          // ---- u = kf + K x ----
-          double uk[NU];
+        // ---- u = kf + K x ----
+        double uk[NU];
 #pragma unroll
-          for (int m = 0; m < NU; ++m) {
-            double v = 0.0;
+        for (int m = 0; m < NU; ++m) {
+          double v = 0.0;
 #pragma unroll
-            for (int q = 0; q < RX; ++q) v += gl * RX + q < NX ? Kcol[q][m] * xk[gl * RX + q < NX ? gl * RX + q : 0] : 0.0;
-            uk[m] = kfu[m] + ex.tsum(v);
-          }
-          if (mine && gl == 0)
+          for (int q = 0; q < RX; ++q) v += gl * RX + q < NX ? Kcol[q][m] * xk[gl * RX + q < NX ? gl * RX + q : 0] : 0.0;
+          uk[m] = kfu[m] + ex.tsum(v);
+        }
+        if (gl == 0)
 #pragma unroll
-            for (int m = 0; m < NU; ++m) o[P.oU + u * NU + m] = uk[m];
-          // ---- x_next = A x + B u (+ e), own rows, then gather ----
-          double xn[RX];
+          for (int m = 0; m < NU; ++m) o[P.oU + u * NU + m] = uk[m];
+        // ---- x_next = A x + B u (+ e), own rows, then gather ----
+        double xn[RX];
+#pragma unroll
+        for (int q = 0; q < RX; ++q) {
+          double v = 0.0;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) v += Arow[q][j] * xk[j];
+#pragma unroll
+          for (int m = 0; m < NU; ++m) v += Brow[q][m] * uk[m];
+          xn[q] = v;
+        }
+        if (jn < len - 1 || leaf) {
 #pragma unroll
           for (int q = 0; q < RX; ++q) {
-            double v = 0.0;
-#pragma unroll
-            for (int j = 0; j < NX; ++j) v += Arow[q][j] * xk[j];
-#pragma unroll
-            for (int m = 0; m < NU; ++m) v += Brow[q][m] * uk[m];
-            xn[q] = v;
+            const int i = gl * RX + q;
+            xn[q] += en[q];
+            if (i < NX) o[P.oX + (k + 1) * NX + i] = xn[q];
           }
-          if (!last) {
+          task_gather<NX, RX, W>(ex, xn, xk);
+        } else {
+          for (int ci = 0; ci < P.m; ++ci) {
+            const int c = t.br_ndx[c0 + ci];
 #pragma unroll
             for (int q = 0; q < RX; ++q) {
               const int i = gl * RX + q;
-              xn[q] += en[q];
-              if (mine && i < NX) o[P.oX + (k + 1) * NX + i] = xn[q];
-            }
-          } else if (mine) {
-            for (int ci = 0; ci < P.m; ++ci) {
-              const int c = t.br_ndx[c0 + ci];
-#pragma unroll
-              for (int q = 0; q < RX; ++q) {
-                const int i = gl * RX + q;
-                if (i < NX) o[P.oX + c * NX + i] = xn[q] + ee[c * NX + i];
-              }
+              if (i < NX) o[P.oX + c * NX + i] = xn[q] + ee[c * NX + i];
             }
           }
-          double xf[NX];
-          task_gather<NX, RX, W>(ex, xn, xf);
-#pragma unroll
-          for (int j = 0; j < NX; ++j) xk[j] = ex.qprev(xf[j], G, gq);
         }
       }
     }
@@ -2204,63 +2115,32 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   BMPC_TOC(C.ws, L, PROF_X3, t_fw);
   BMPC_TIC(t_post);
   // ---- post-pass: nu_k = -(l_k + P_k x_k), slack recovery -----------------------------------
-  // right-hand sides four per pass: a node's P row, dh and slack weights are loaded once for
-  // the four (the coupling solve's nc + 2 right-hand sides re-read them per rhs otherwise);
-  // every value is formed exactly as one rhs per pass forms it
-  constexpr int RB = 4;
-  struct VR { double v[RB]; };
-  for (int rb = 0; rb < nr; rb += RB) {
-    const int rn = nr - rb < RB ? nr - rb : RB;
+  for (int ri = 0; ri < nr; ++ri) {
+    gdouble* o = o0 + ri * os;
+    const gdouble* rr = r0 + ri * rs;
+    const gdouble* lvec = lv_ + ri * lstr;
     if (n0) {
+      gdouble* nn = n0 + ri * ns;
+      const bool lon = ex.uniform(ri >= ncw);   // Woodbury columns: l = 0 off the column's root path
       lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
         const int k = it / NX, i = it % NX;
-        double pr[NX];
+        double v = (lon || needed(t.x_branch[k], ri)) ? lvec[it] : 0.0;
 #pragma unroll
-        for (int j = 0; j < NX; ++j) pr[j] = ws[L.P + k * NX * NX + i * NX + j];
-        VR out;
-#pragma unroll
-        for (int a2 = 0; a2 < RB; ++a2) {
-          const int ri = rb + (a2 < rn ? a2 : 0);
-          const gdouble* o = o0 + ri * os;
-          // Woodbury columns: l = 0 off the column's root path
-          double v = (ri >= ncw || needed(t.x_branch[k], ri)) ? lv_[ri * lstr + it] : 0.0;
-#pragma unroll
-          for (int j = 0; j < NX; ++j) v += pr[j] * o[P.oX + k * NX + j];
-          out.v[a2] = -v;
-        }
-        return out;
-      }, [&](int it, const VR& r) {
-#pragma unroll
-        for (int a2 = 0; a2 < RB; ++a2)
-          if (a2 < rn) n0[(rb + a2) * ns + it] = r.v[a2];
-      });
+        for (int j = 0; j < NX; ++j) v += ws[L.P + k * NX * NX + i * NX + j] * o[P.oX + k * NX + j];
+        return -v;
+      }, [&](int it, double v) { nn[it] = v; });
     }
     lane_batch<BMPC_TS_UN>(ex, 0, P.T * Nc, [&](int it) {
       const int k = it / Nc, c = it % Nc;
       const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // branch-free: terminal nodes add 0
-      double cf[NX];
+      double fx = 0.0;
 #pragma unroll
       for (int j = 0; j < NX; ++j) {   // -dh for c == 0, Fx[c-1] otherwise (blend: no branch around the dh load)
         const double dhv = dh[k * NX + j], fxj = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
-        cf[j] = m0 * (-dhv) + (1.0 - m0) * fxj;
+        fx += (m0 * (-dhv) + (1.0 - m0) * fxj) * o[P.oX + k * NX + j];
       }
-      const double s1 = sdv[it * 2 + 1], s0 = sdv[it * 2];
-      VR out;
-#pragma unroll
-      for (int a2 = 0; a2 < RB; ++a2) {
-        const int ri = rb + (a2 < rn ? a2 : 0);
-        const gdouble* o = o0 + ri * os;
-        double fx = 0.0;
-#pragma unroll
-        for (int j = 0; j < NX; ++j) fx += cf[j] * o[P.oX + k * NX + j];
-        out.v[a2] = (r0[ri * rs + P.oS + it] + s1 * on * fx) / s0;
-      }
-      return out;
-    }, [&](int it, const VR& r) {
-#pragma unroll
-      for (int a2 = 0; a2 < RB; ++a2)
-        if (a2 < rn) o0[(rb + a2) * os + P.oS + it] = r.v[a2];
-    });
+      return (rr[P.oS + it] + sdv[it * 2 + 1] * on * fx) / sdv[it * 2];
+    }, [&](int it, double v) { o[P.oS + it] = v; });
   }
   ex.sync();
   BMPC_TOC(C.ws, L, PROF_X4, t_post);

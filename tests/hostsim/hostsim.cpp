@@ -35,8 +35,6 @@ struct HostExecT {
   const int32_t* tab = nullptr;   // ... and for its LDS copy of the topology tables
   double* eco = nullptr;      // ... and for the per-ego constants (kTransform)
   static constexpr int kTaskLanes = 1;
-  static constexpr int kChainQuads = 1;   // one task per lane group, no chain hops
-  double qprev(double v, int, int) const { return v; }
   // one lane holds a whole cone (fused IPM passes); -DBMPC_HOST_CONE_REGS=1 runs the unfused
   // chain instead (what the GPU takes for cones wider than 8 rows per group lane)
   static constexpr int kConeRegRows = BMPC_HOST_CONE_REGS;
