@@ -128,7 +128,7 @@ struct Plan {
   int ng;     // number of "global" variables (rho, sigma, mu+, mu-, J)
   int nsm;    // dense coupling system size
   // per-wave LDS scratch (doubles): coupling matrix, pivots, rhs, reduction slots
-  int lds_M, lds_piv, lds_rhs, lds_red, nlds;
+  int lds_M, lds_piv, lds_rhs, lds_rhs2, lds_red, nlds;   // lds_rhs2: the second rhs of a paired back half
   // plan-constant matrices in LDS, read with lane-varying rows (a lane-varying index into the
   // constant buffer is a vector memory round trip): W1 (n x n), Wu (d x d), Fx (nFx x n), Fu (nFu x d)
   int lds_w, lds_wu, lds_fx, lds_fu, nconst;

@@ -18,6 +18,9 @@
 
 #include "bmpc_tree.h"
 
+#ifndef BMPC_PAIR_BACK
+#define BMPC_PAIR_BACK 1     // kkt_solve_pair's two back halves in one pass over the Woodbury data
+#endif
 #ifndef BMPC_TS_UN
 #define BMPC_TS_UN 2         // elements per lane batch in the tree solve's slack pre- / post-passes (2: -1.1% k_ipm vs 4, 8: +15%)
 #endif
@@ -216,6 +219,46 @@ BMPC_HD void cone_supp_gdx(const X& ex, CPlan& P, const T& t, const gdouble* g0,
       for (int j = 0; j < 16; ++j) acc[j] += (kk[u] == j ? gv[u] : 0.0) * xv[u];
   }
   ex.template sum_n<16>(acc);
+}
+
+// cone_supp_gdx for two vectors at once (each g_k entry loaded once for both); per vector the
+// same products and sums as cone_supp_gdx
+template <class X, class T>
+BMPC_HD void cone_supp_gdx2(const X& ex, CPlan& P, const T& t, const gdouble* g0, size_t gstr, const gdouble* dx1,
+                            const gdouble* dx2, int k0, double (&acc1)[16], double (&acc2)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc1[j] = 0.0, acc2[j] = 0.0;
+  const int nc = P.ncones;
+  const int kn = nc - k0 < 16 ? nc - k0 : 16;
+  const int full = P.N * (P.n + P.d + P.Nc);
+  int tot = 0;
+  for (int j = 0; j < kn; ++j) tot += cone_supp_len(P, t, k0 + j);
+  constexpr int UN = 4;
+  for (int b = ex.lane; b < tot; b += UN * ex.nlanes) {
+    double gv[UN], xv1[UN], xv2[UN];
+    int kk[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int f = b + u * ex.nlanes < tot ? b + u * ex.nlanes : b;
+      const int j = f / full < kn ? f / full : kn - 1;
+      const int e = f - j * full;
+      const int i = cone_supp_idx(P, t, k0 + j, e);
+      kk[u] = b + u * ex.nlanes < tot ? j : -1;
+      gv[u] = g0[(size_t)(k0 + j) * gstr + i];
+      xv1[u] = dx1[i];
+      xv2[u] = dx2[i];
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double g = kk[u] == j ? gv[u] : 0.0;
+        acc1[j] += g * xv1[u];
+        acc2[j] += g * xv2[u];
+      }
+  }
+  ex.template sum_n<16>(acc1);
+  ex.template sum_n<16>(acc2);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2474,6 +2517,107 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
   else apply_G<X, NX, NU, 1>(ex, C, dx, dzh, r3h, tr);
 }
 
+// kkt_back for the pair's two directions (kkt_solve_pair: the c and affine solves) at once:
+// each g_k and Woodbury column is loaded once for both; per direction every value is formed as
+// kkt_back forms it (same products, same order).  The second right-hand side of the coupling
+// solve sits at Plan::lds_rhs2.
+template <class X, int NX, int NU>
+BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const gdouble* r21, const gdouble* r3h1,
+                           gdouble* dx1, gdouble* dy1, gdouble* dzh1, const gdouble* tz2, const gdouble* r22,
+                           const gdouble* r3h2, gdouble* dx2, gdouble* dy2, gdouble* dzh2, bool fin) {
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* tr = ws + L.k_r0;
+  const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
+  auto* b1 = coup_vec(ex, P.lds_rhs);
+  auto* b2 = coup_vec(ex, P.lds_rhs2);
+  const gdouble* eta = ws + L.eta;
+  if (coup_supp_dots(P)) {   // g_k' dx over each cone's support, sixteen cones per pass
+    const auto t = topo_view(P, ex);
+    for (int k0 = 0; k0 < nc; k0 += 16) {
+      double acc1[16], acc2[16];
+      cone_supp_gdx2(ex, P, t, ws + L.gk, P.nv, dx1, dx2, k0, acc1, acc2);
+      if (ex.lane == 0)
+        for (int a = 0; a < 16 && k0 + a < nc; ++a) {
+          b1[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc1[a];
+          b2[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc2[a];
+        }
+    }
+  } else {
+    for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx1 and g_k' dx2, four cones per pass
+      const int na = nc - k0 < 4 ? nc - k0 : 4;
+      double acc[4][4];
+      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx1, (size_t)(dx2 - dx1), 2, 0, P.oRho, P.oS, P.oJ,
+                 acc);
+      if (ex.lane == 0)
+        for (int a = 0; a < na; ++a) {
+          b1[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
+          b2[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][1];
+        }
+    }
+  }
+  for (int i = ex.lane; i < ng + nb; i += ex.nlanes) {
+    b1[i] = i < ng ? tz1[gvar(P, i)] : r21[P.T * NX + i - ng];
+    b2[i] = i < ng ? tz2[gvar(P, i)] : r22[P.T * NX + i - ng];
+  }
+  ex.sync();
+  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b1, ns);
+  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b2, ns);
+  const auto* bc1 = b1 + ng + nb;
+  const auto* bc2 = b2 + ng + nb;
+  const gdouble* colk = ws + L.colk;
+  const gdouble* colnu = ws + L.colnu;
+  const int n1 = P.oRho, n2 = n1 + (P.oJ - P.oS), n3 = n2 + P.T * NX;
+  auto row = [&](int t, int& i, bool& isx) {
+    isx = t < n2;
+    i = t < n1 ? t : t < n2 ? P.oS + (t - n1) : t - n2;
+  };
+  struct V2 { double a, b; };
+  lane_batch<4>(ex, 0, n3, [&](int t) {
+    int i;
+    bool isx;
+    row(t, i, isx);
+    const gdouble* col = isx ? colk : colnu;
+    const size_t cs = isx ? (size_t)P.nv : (size_t)P.neq;
+    const gdouble* s1 = isx ? dx1 : dy1;
+    const gdouble* s2 = isx ? dx2 : dy2;
+    double v1 = s1[i], v2 = s2[i];
+    for (int k0 = 0; k0 < nc; k0 += 4) {
+      double c4[4], p4[4], q4[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        c4[a] = col[(size_t)(k0 + a < nc ? k0 + a : nc - 1) * cs + i];
+        p4[a] = k0 + a < nc ? bc1[k0 + a] : 0.0;
+        q4[a] = k0 + a < nc ? bc2[k0 + a] : 0.0;
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) v1 -= p4[a] * c4[a];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) v2 -= q4[a] * c4[a];
+    }
+    return V2{v1, v2};
+  }, [&](int t, V2 v) {
+    int i;
+    bool isx;
+    row(t, i, isx);
+    if (isx) dx1[i] = v.a, dx2[i] = v.b;
+    else dy1[i] = v.a, dy2[i] = v.b;
+  });
+  for (int i = ex.lane; i < ng + nb; i += ex.nlanes) {
+    if (i < ng) dx1[gvar(P, i)] = b1[i], dx2[gvar(P, i)] = b2[i];
+    else dy1[P.T * NX + i - ng] = b1[i], dy2[P.T * NX + i - ng] = b2[i];
+  }
+  ex.sync();
+  if (fin) {
+    apply_G<X, NX, NU, 2>(ex, C, dx1, dzh1, r3h1, tr);
+    apply_G<X, NX, NU, 2>(ex, C, dx2, dzh2, r3h2, tr);
+  } else {
+    apply_G<X, NX, NU, 1>(ex, C, dx1, dzh1, r3h1, tr);
+    apply_G<X, NX, NU, 1>(ex, C, dx2, dzh2, r3h2, tr);
+  }
+}
+
 template <class X, int NX, int NU>
 BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdouble* r2, const gdouble* r3h,
                         gdouble* dx, gdouble* dy, gdouble* dz, int nitref);
@@ -2585,8 +2729,12 @@ BMPC_FN bool kkt_solve_pair(const X ex, const Ctx Cin, const gdouble* r1c, const
   gdouble* x2 = ws + L.x2;
   gdouble* y2 = ws + L.y2;
   gdouble* z2 = ws + L.z2;
+#if BMPC_PAIR_BACK
+  kkt_back_pair<X, NX, NU>(ex, C, tzc, bv, r3hc, x1, y1, z1, tza, ry, r3ha, x2, y2, z2, fin);
+#else
   kkt_back<X, NX, NU, false>(ex, C, tzc, bv, r3hc, x1, y1, z1, fin);
   kkt_back<X, NX, NU, false>(ex, C, tza, ry, r3ha, x2, y2, z2, fin);
+#endif
   if (fin) return true;
   kkt_refine<X, NX, NU>(ex, C, r1c, bv, r3hc, x1, y1, z1, nitref);
   kkt_refine<X, NX, NU>(ex, C, r1a, ry, r3ha, x2, y2, z2, nitref);

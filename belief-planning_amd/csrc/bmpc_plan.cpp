@@ -325,11 +325,12 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.lds_scr = std::max(64, (P.nconst + 7) & ~7);
   // (plans whose staging does not fit form each node's slack terms inside the tree solve's sweep)
   P.nscr = desc.controller == BMPC_CTRL_CVAR && P.lds_scr + ncoup + T * P.Nc <= 1248 ? T * P.Nc : 0;
-  // pivots and right-hand side before the matrix: lean launches keep those two in LDS too (the
+  // pivots and right-hand sides before the matrix: lean launches keep those in LDS too (the
   // substitutions' dependent chains then run on LDS; only the matrix moves to the slab)
   P.lds_piv = P.lds_scr + P.nscr;
   P.lds_rhs = P.lds_piv + P.nsm;
-  P.lds_M = P.lds_rhs + P.nsm;
+  P.lds_rhs2 = P.lds_rhs + P.nsm;   // the pair's second right-hand side (kkt_back_pair)
+  P.lds_M = P.lds_rhs2 + P.nsm;
   P.nlds = P.lds_M + P.nsm * P.nsm;
   P.nlds_lean = P.lds_M;
 
