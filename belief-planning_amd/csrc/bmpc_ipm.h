@@ -1928,18 +1928,41 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
     for (int ri = 0; ri < nr; ++ri) {
       const gdouble* rr = r0 + ri * rs;
       gdouble* q0 = q0_ + ri * lstr;
-      lane_batch<BMPC_TS_UN_AV>(ex, 0, P.T * Nc, [&](int it) {
-        const int k = it / Nc;
+      // the nodes whose q0 the backward sweep reads: all of them, or for a Woodbury column only
+      // the nodes of its cone's root path (up to four branches, s_h / l_h: first node / count)
+      int s0 = 0, l0 = P.T, s1 = 0, l1 = 0, s2 = 0, l2 = 0, s3 = 0, l3 = 0;
+      if (ri < ncw) {
+        int c = t.cone_c[ri] < 0 ? 0 : t.cone_c[ri];
+        int st[4] = {0, 0, 0, 0}, ln[4] = {0, 0, 0, 0};
+        bool deeper = true;   // (deeper trees keep the whole range)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (deeper) {
+            st[q] = t.br_ndx[c];
+            ln[q] = t.br_len[c] + (t.br_child0[c] < 0 ? 1 : 0);   // a leaf's terminal node
+            if (c == 0) deeper = false;
+            else c = (c - 1) / P.m;
+          }
+        }
+        if (!deeper) s0 = st[0], l0 = ln[0], s1 = st[1], l1 = ln[1], s2 = st[2], l2 = ln[2], s3 = st[3], l3 = ln[3];
+      }
+      const int nn = l0 + l1 + l2 + l3;
+      auto node = [&](int f) {   // the f-th node of the ranges (branch-free)
+        const int f1 = f - l0, f2 = f1 - l1, f3 = f2 - l2;
+        return f < l0 ? s0 + f : f1 < l1 ? s1 + f1 : f2 < l2 ? s2 + f2 : s3 + f3;
+      };
+      lane_batch<BMPC_TS_UN_AV>(ex, 0, nn * Nc, [&](int f) {
+        const int k = node(f / Nc), it = k * Nc + f % Nc;
         const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;   // terminal nodes add 0
         return on * sdv[it * 2 + 1] * rr[P.oS + it] / sdv[it * 2];
-      }, [&](int it, double v) { av[it] = v; });
+      }, [&](int f, double v) { av[node(f / Nc) * Nc + f % Nc] = v; });
       ex.sync();
-      lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
-        const int k = it / NX, j = it % NX;
+      lane_batch<BMPC_TS_UN>(ex, 0, nn * NX, [&](int f) {
+        const int k = node(f / NX), j = f % NX, it = k * NX + j;
         double v = -rr[P.oX + it] + dh[it] * av[k * Nc];
         for (int c = 1; c < Nc; ++c) v -= fxv(P, ex, c - 1, j) * av[k * Nc + c];
         return v;
-      }, [&](int it, double v) { q0[it] = v; });
+      }, [&](int f, double v) { q0[node(f / NX) * NX + f % NX] = v; });
       ex.sync();
     }
     BMPC_TOC(C.ws, L, PROF_X1, t_pre);
