@@ -4,6 +4,8 @@
 # 4096-ego batch compared with mode 0, interleaved timings, a rocprofv3 kernel trace of mode 1
 # (per-phase kernel times) and FETCH_SIZE / WRITE_SIZE of every mode (per phase for mode 1).
 # usage: TAG=r03f MODES="0 1 2 1s4" bash tools/ab_phased.sh   (MsN: mode M with BMPC_PH_STREAMS=N)
+# the modes live in a tools-only build: python tools/build_variant.py ph -DBMPC_WITH_PHASED, then
+# BMPC_LIBRARY=$PWD/belief-planning_amd/libbmpc_ph.so
 set -o pipefail
 tag=${TAG:-abph}
 modes=${MODES:-0 1 2}
