@@ -57,3 +57,22 @@ def test_desc_struct_layout_matches_header():
     assert offmc == abi.PlanDesc.mc.offset
     assert psize == C.sizeof(abi.Policy)
     assert offfl == abi.PlanDesc.flags.offset
+
+
+def test_alternate_builds_load_non_strictly(tmp_path):
+    """The product library binds every entry point or fails; another build named by
+    BMPC_LIBRARY (an older source in an A/B) loads without the ones it lacks, which then
+    raise BmpcUnavailable when called."""
+    import subprocess
+    import pytest
+    from bmpc import _lib
+    src = tmp_path / "old.c"
+    src.write_text("int bmpc_abi_version(void) { return 2; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)])
+    with pytest.raises(AttributeError):
+        _lib.load(str(so))
+    lib = _lib.load(str(so), strict=False)
+    assert lib.bmpc_abi_version() == 2
+    with pytest.raises(_lib.BmpcUnavailable):
+        lib.bmpc_set_lane_ref(None, 0, None, None)
