@@ -18,6 +18,9 @@
 
 #include "bmpc_tree.h"
 
+#ifndef BMPC_PAIR_REFINE
+#define BMPC_PAIR_REFINE 1   // the pair's refinement rounds share their correction tree solves
+#endif
 #ifndef BMPC_PAIR_BACK
 #define BMPC_PAIR_BACK 1     // kkt_solve_pair's two back halves in one pass over the Woodbury data
 #endif
@@ -2544,7 +2547,7 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
 // each g_k and Woodbury column is loaded once for both; per direction every value is formed as
 // kkt_back forms it (same products, same order).  The second right-hand side of the coupling
 // solve sits at Plan::lds_rhs2.
-template <class X, int NX, int NU>
+template <class X, int NX, int NU, bool R3ZERO = false>
 BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const gdouble* r21, const gdouble* r3h1,
                            gdouble* dx1, gdouble* dy1, gdouble* dzh1, const gdouble* tz2, const gdouble* r22,
                            const gdouble* r3h2, gdouble* dx2, gdouble* dy2, gdouble* dzh2, bool fin) {
@@ -2632,7 +2635,10 @@ BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const g
     else dy1[P.T * NX + i - ng] = b1[i], dy2[P.T * NX + i - ng] = b2[i];
   }
   ex.sync();
-  if (fin) {
+  if constexpr (R3ZERO) {
+    apply_G<X, NX, NU, 3>(ex, C, dx1, dzh1, r3h1, tr);
+    apply_G<X, NX, NU, 3>(ex, C, dx2, dzh2, r3h2, tr);
+  } else if (fin) {
     apply_G<X, NX, NU, 2>(ex, C, dx1, dzh1, r3h1, tr);
     apply_G<X, NX, NU, 2>(ex, C, dx2, dzh2, r3h2, tr);
   } else {
@@ -2681,27 +2687,32 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
   gdouble* cy = ws + L.k_cy;
   gdouble* cz = ws + L.k_cz;
   gdouble* tv = ws + L.k_nv1;
-  const double sc = nitref == 0 ? 0.0 : ex.max(fmax(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(r1[i]); }),
-                                     strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(r2[i]); })),
-                                strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); })));
+  // the scale max(|r1|, |r2|, |r3h|) and the residual's max norm are taken in the passes that
+  // read r1 / r2 and write e1 / e2 (max is exact: the same values as separate passes); the |r3h|
+  // part before the first round
+  double msc = nitref == 0 ? 0.0 : strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); });
+  double sc = 0.0;
   for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     ProfScope _pr(C.ws, L.prof, PROF_REFINE);
 #endif
+    double merr = -1e300;
     // e1 = r1 - A'dy - G'W^-1 dzh
     apply_W(ex, C, 1, dz, e3);
     apply_GT<X, NX, NU>(ex, C, e3, tv);
     apply_AT<X, NX, NU>(ex, C, dy, e1);
-    lane_batch<16>(ex, 0, P.nv, [&](int i) { return r1[i] - e1[i] - tv[i]; }, [&](int i, double v) { e1[i] = v; });
+    lane_batch<16>(ex, 0, P.nv, [&](int i) { const double a = r1[i]; msc = fmax(msc, fabs(a)); return a - e1[i] - tv[i]; },
+                   [&](int i, double v) { e1[i] = v; merr = fmax(merr, fabs(v)); });
     // e2 = r2 - A dx
     apply_A<X, NX, NU>(ex, C, dx, e2);
-    lane_batch(ex, 0, P.neq, [&](int i) { return r2[i] - e2[i]; }, [&](int i, double v) { e2[i] = v; });
+    lane_batch(ex, 0, P.neq, [&](int i) { const double a = r2[i]; msc = fmax(msc, fabs(a)); return a - e2[i]; },
+               [&](int i, double v) { e2[i] = v; merr = fmax(merr, fabs(v)); });
     // e3 = r3h - W^-1 G dx + dzh is zero up to rounding: kkt_solve_once computed dzh as
     // W^-1 G dx - r3h from the final dx with the same operators (the correction solve takes
     // r3h = 0 without a vector)
+    if (itr == 0) sc = ex.max(msc);
+    const double err = ex.max(merr);
     ex.sync();
-    const double err = ex.max(fmax(strided_partial<8, 1>(ex.lane, ex.nlanes, P.nv, [&](int i) { return fabs(e1[i]); }),
-                                   strided_partial<8, 1>(ex.lane, ex.nlanes, P.neq, [&](int i) { return fabs(e2[i]); })));
 #ifdef BMPC_HOST_DEBUG
     printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
 #endif
@@ -2714,6 +2725,87 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
   }
   // dz = W^-1 dzh (in place)
   apply_W(ex, C, 1, dz, dz);
+}
+
+// kkt_refine of the pair's two directions in lock step: while both refine, their correction
+// solves share one tree solve (two right-hand sides) and one paired back half; a direction whose
+// residual met the tolerance stops as kkt_refine stops it.  Each direction's operations are
+// kkt_refine's, in the same order (its scratch: the second halves of k_e1 / k_e2 / k_cx /
+// k_cy / k_cz).
+template <class X, int NX, int NU>
+BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, const gdouble* r2a, const gdouble* r3ha,
+                             gdouble* dxa, gdouble* dya, gdouble* dza, const gdouble* r1b, const gdouble* r2b,
+                             const gdouble* r3hb, gdouble* dxb, gdouble* dyb, gdouble* dzb, int nitref) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, neq = P.neq, nr = P.nrows;
+  gdouble* e3 = ws + L.k_e3;
+  gdouble* tv = ws + L.k_nv1;
+  const gdouble* r1[2] = {r1a, r1b};
+  const gdouble* r2[2] = {r2a, r2b};
+  const gdouble* r3h[2] = {r3ha, r3hb};
+  gdouble* dx[2] = {dxa, dxb};
+  gdouble* dy[2] = {dya, dyb};
+  gdouble* dz[2] = {dza, dzb};
+  double sc[2] = {0.0, 0.0};
+  double msc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)   // kkt_refine's scale and residual norms, per direction
+    msc[j] = nitref == 0 ? 0.0 : strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[j][i]); });
+  bool on[2] = {true, true};
+  for (int itr = 0; itr < nitref; ++itr) {
+#if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+    ProfScope _pr(C.ws, L.prof, PROF_REFINE);
+#endif
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (!ex.uniform(on[j])) continue;
+      gdouble* e1 = ws + L.k_e1 + j * nv;
+      gdouble* e2 = ws + L.k_e2 + j * neq;
+      double merr = -1e300;
+      apply_W(ex, C, 1, dz[j], e3);
+      apply_GT<X, NX, NU>(ex, C, e3, tv);
+      apply_AT<X, NX, NU>(ex, C, dy[j], e1);
+      lane_batch<16>(ex, 0, P.nv, [&](int i) { const double a = r1[j][i]; msc[j] = fmax(msc[j], fabs(a)); return a - e1[i] - tv[i]; },
+                     [&](int i, double v) { e1[i] = v; merr = fmax(merr, fabs(v)); });
+      apply_A<X, NX, NU>(ex, C, dx[j], e2);
+      lane_batch(ex, 0, P.neq, [&](int i) { const double a = r2[j][i]; msc[j] = fmax(msc[j], fabs(a)); return a - e2[i]; },
+                 [&](int i, double v) { e2[i] = v; merr = fmax(merr, fabs(v)); });
+      if (itr == 0) sc[j] = ex.max(msc[j]);
+      const double err = ex.max(merr);
+      ex.sync();
+      on[j] = ex.uniform(err > BMPC_REFTOL * fmax(sc[j], 1.0));
+    }
+    if (!ex.uniform(on[0] || on[1])) break;
+    gdouble* cx = ws + L.k_cx;
+    gdouble* cy = ws + L.k_cy;
+    gdouble* cz = ws + L.k_cz;
+    if (ex.uniform(on[0] && on[1])) {   // both corrections: one tree solve, one back half
+      tree_solve<X, NX, NU>(ex, C, 2, ws + L.k_e1, nv, ws + L.k_e2, neq, cx, nv, cy, neq);
+      kkt_back_pair<X, NX, NU, true>(ex, C, ws + L.k_e1, ws + L.k_e2, nullptr, cx, cy, cz, ws + L.k_e1 + nv,
+                                     ws + L.k_e2 + neq, nullptr, cx + nv, cy + neq, cz + nr, false);
+    } else {
+      const int j = on[0] ? 0 : 1;
+      kkt_solve_once<X, NX, NU, true>(ex, C, ws + L.k_e1 + j * nv, ws + L.k_e2 + j * neq, nullptr, cx + j * nv,
+                                      cy + j * neq, cz + j * nr, false, false);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (!ex.uniform(on[j])) continue;
+      const gdouble* cxj = cx + j * nv;
+      const gdouble* cyj = cy + j * neq;
+      const gdouble* czj = cz + j * nr;
+      lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[j][i] + cxj[i]; }, [&](int i, double v) { dx[j][i] = v; });
+      lane_batch(ex, 0, P.neq, [&](int i) { return dy[j][i] + cyj[i]; }, [&](int i, double v) { dy[j][i] = v; });
+      lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[j][i] + czj[i]; }, [&](int i, double v) { dz[j][i] = v; });
+      ex.sync();
+    }
+  }
+  // dz = W^-1 dzh (in place)
+  apply_W(ex, C, 1, dza, dza);
+  apply_W(ex, C, 1, dzb, dzb);
 }
 
 // The two KKT solves of an IPM iteration that need only the factorisation -- the c direction
@@ -2759,8 +2851,12 @@ BMPC_FN bool kkt_solve_pair(const X ex, const Ctx Cin, const gdouble* r1c, const
   kkt_back<X, NX, NU, false>(ex, C, tza, ry, r3ha, x2, y2, z2, fin);
 #endif
   if (fin) return true;
+#if BMPC_PAIR_REFINE
+  kkt_refine_pair<X, NX, NU>(ex, C, r1c, bv, r3hc, x1, y1, z1, r1a, ry, r3ha, x2, y2, z2, nitref);
+#else
   kkt_refine<X, NX, NU>(ex, C, r1c, bv, r3hc, x1, y1, z1, nitref);
   kkt_refine<X, NX, NU>(ex, C, r1a, ry, r3ha, x2, y2, z2, nitref);
+#endif
   return true;
 }
 

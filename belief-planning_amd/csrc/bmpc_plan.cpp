@@ -414,14 +414,14 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.bestx = take(nv);
   L.k_r0 = take(nr);
   L.k_nv0 = take(nv);
-  L.k_e1 = take(nv);
-  L.k_e2 = take(neq);
+  L.k_e1 = take(2 * (size_t)nv);    // two halves: the pair's refinement (kkt_refine_pair)
+  L.k_e2 = take(2 * (size_t)neq);
   L.k_e3 = take(nr);
   L.k_t3 = take(nr);
   L.k_t3b = take(nr);
-  L.k_cx = take(nv);
-  L.k_cy = take(neq);
-  L.k_cz = take(nr);
+  L.k_cx = take(2 * (size_t)nv);
+  L.k_cy = take(2 * (size_t)neq);
+  L.k_cz = take(2 * (size_t)nr);
   L.k_nv1 = take(nv);
   L.dl = take(P.nlp);
   L.dli = take(P.nlp);

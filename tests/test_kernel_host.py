@@ -116,3 +116,47 @@ def test_unfused_cone_chain_replays_reference():
     env = dict(os.environ, BMPC_HOSTSIM_FLAGS="-DBMPC_HOST_CONE_REGS=1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def _seeded_closed_loop(flags, B, N, NB, steps=2):
+    """J / status / iters / uPred of a seeded batch over a few closed-loop steps, from a host
+    build with extra -D flags (its own process: hostsim_lib reads the flags at import)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    here = os.path.dirname(__file__)
+    repo = os.path.dirname(here)
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r, %r]\n"
+        "import hostsim_lib as H\n"
+        "from common import highway_desc, highway_policy_rows, seeded_batch\n"
+        "x, z, xref, tgt = seeded_batch(%d, 0)\n"
+        "hs = H.HostSim(highway_desc(%d, %d), %d); hs.set_policies(highway_policy_rows(tgt)); out = {}\n"
+        "for s in range(%d):\n"
+        "    r = hs.solve(x, z, xref)\n"
+        "    for k in ('J', 'status', 'iters', 'upred'): out[k + str(s)] = np.asarray(r[k]).copy()\n"
+        "    u0 = r['upred'][:, 0]\n"
+        "    x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)\n"
+        "    z = z + 0.1 * np.stack([z[:, 2], 0 * z[:, 0], 0 * z[:, 0], 0 * z[:, 0]], 1)\n"
+        "np.savez(sys.argv[1], **out)\n") % (here, repo, os.path.join(repo, "belief-planning_amd"), B, N, NB, B, steps)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "o.npz")
+        env = dict(os.environ, BMPC_HOSTSIM_FLAGS=flags)
+        r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        import numpy as np
+        return dict(np.load(path))
+
+
+def test_paired_solves_are_bit_identical():
+    """The pair's back halves in one pass (BMPC_PAIR_BACK) and its refinement rounds in shared
+    tree solves (BMPC_PAIR_REFINE) form every value as the per-direction code does: a host build
+    without them gives the same bits over closed-loop steps (N=20 NB=1: block dot products;
+    N=8 NB=2: per-cone support products)."""
+    import numpy as np
+    for B, N, NB in ((24, 20, 1), (8, 8, 2)):
+        a = _seeded_closed_loop("", B, N, NB)
+        b = _seeded_closed_loop("-DBMPC_PAIR_BACK=0 -DBMPC_PAIR_REFINE=0", B, N, NB)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (N, NB, k)
