@@ -48,6 +48,7 @@ struct DevExecT {
   static constexpr int nlanes = 64;
   // one wave runs a band QP: blocked factorisation and sweeps on wave broadcasts (bmpc_bandqp.h)
   static constexpr bool kBqpWave = true;
+  static constexpr bool kInlineG = true;    // apply_G inline (bmpc_ipm.h)
   // small dense systems with a lane per row (bmpc_ipm.h, small_lu_solve_rows)
   static constexpr bool kRowLanes = true;
   // lane l's v, wave-uniform (l uniform)

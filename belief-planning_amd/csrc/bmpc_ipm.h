@@ -364,9 +364,21 @@ BMPC_HD double cone_row0(const X& ex, const ConeGroups& G, const double (&v)[UC]
 // out(rows) = G zv, cone rows boosted.  WM = 1: out = W^-1 (G zv) - r3h, WM = 2: out =
 // W^-1 (W^-1 (G zv) - r3h), WM = 3: out = W^-1 (G zv) -- the tail of kkt_solve_once without the
 // G dx vector in the slab (tr: scratch of the unfused chain).
+//
+// Executors with kInlineG (the one-wave kernels) take it inline: its callers already hold the
+// registers an out-of-line apply_G saves and restores on every call (-3% bytes, -1% k_ipm at
+// 4,096 egos, profiles/r04/r04y_inline_apply_g_*.log); the multi-wave kernel calls it out of line
+// (one-ego latency +2-3% inline).
+template <class X, class = void>
+struct inline_g { static constexpr bool value = false; };
+template <class X>
+struct inline_g<X, decltype((void)X::kInlineG)> { static constexpr bool value = X::kInlineG; };
 template <class X, int NX, int NU, int WM = 0>
-BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out, const gdouble* r3h = nullptr,
-                             gdouble* tr = nullptr) {
+BMPC_HD void apply_G(const X ex, const Ctx& C, const gdouble* zv, gdouble* out, const gdouble* r3h = nullptr,
+                     gdouble* tr = nullptr);
+template <class X, int NX, int NU, int WM>
+BMPC_HD void apply_G_body(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out, const gdouble* r3h,
+                          gdouble* tr) {
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   if constexpr (WM > 0) {
@@ -573,6 +585,16 @@ BMPC_FN_APPLY_G void apply_G(const X ex, const Ctx Cin, const gdouble* zv, gdoub
   }
   BMPC_TOC(C.ws, *C.L, PROF_G_CONE, t_gcone);
   ex.sync();
+}
+template <class X, int NX, int NU, int WM>
+BMPC_FN_APPLY_G void apply_G_call(const X ex, const Ctx Cin, const gdouble* zv, gdouble* out, const gdouble* r3h,
+                                  gdouble* tr) {
+  apply_G_body<X, NX, NU, WM>(ex, Cin, zv, out, r3h, tr);
+}
+template <class X, int NX, int NU, int WM>
+BMPC_HD void apply_G(const X ex, const Ctx& C, const gdouble* zv, gdouble* out, const gdouble* r3h, gdouble* tr) {
+  if constexpr (inline_g<X>::value) apply_G_body<X, NX, NU, WM>(ex, C, zv, out, r3h, tr);
+  else apply_G_call<X, NX, NU, WM>(ex, C, zv, out, r3h, tr);
 }
 
 // out(nv) = G' r (+ add, when add is not NULL)
