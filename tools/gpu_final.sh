@@ -1,11 +1,12 @@
 #!/bin/bash
-# round-end GPU pass: parity tests, default bench (CPU baselines), config-5 shard size, the
+# round-end GPU pass: parity tests, smoke(), default bench (CPU baselines), config-5 shard size, the
 # BASELINE config sweep, the QP-solver timing, rocprofv3 stats + PMC passes of the bench
 # usage: bash tools/gpu_final.sh TAG
 set -o pipefail
 tag=${1:-r02}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rA --timeout 180 --timeout-method thread > gpurun_out/${tag}_gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || exit $?
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${tag}_bench.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --gpus 1 --global-batch 8192 --no-cpu-baseline > gpurun_out/${tag}_bench_gb8192.log 2>&1 || exit $?
 out=gpurun_out/${tag}_config_sweep.jsonl
