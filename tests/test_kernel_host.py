@@ -149,17 +149,6 @@ def _seeded_closed_loop(flags, B, N, NB, steps=2):
         return dict(np.load(path))
 
 
-def test_batched_post_pass_is_bit_identical():
-    """The tree solve's post-pass four right-hand sides per pass (BMPC_TS_POST_RB_MIN: the
-    NB=2 coupling solve's 15) forms every value as the one-rhs pass: same bits over
-    closed-loop steps as a host build that never batches."""
-    import numpy as np
-    a = _seeded_closed_loop("", 8, 8, 2)
-    b = _seeded_closed_loop("-DBMPC_TS_POST_RB_MIN=1000", 8, 8, 2)
-    for k in a:
-        assert np.array_equal(a[k], b[k]), k
-
-
 def test_paired_solves_are_bit_identical():
     """The pair's back halves in one pass (BMPC_PAIR_BACK) and its refinement rounds in shared
     tree solves (BMPC_PAIR_REFINE) form every value as the per-direction code does: a host build
