@@ -1890,7 +1890,10 @@ BMPC_HD void bw_node(const X& ex, int gl, const double (&qx)[RX], const double (
 // The first ncw right-hand sides are Woodbury cone columns (kkt_coupling): column k is
 // supported on cone k's child branch only, so its backward sweep runs only on that branch and
 // its ancestors (elsewhere l and kf are exactly zero and are not stored or read).
-template <class X, int NX, int NU>
+// RB: the post-pass takes four right-hand sides per pass (a separate instantiation, called by
+// kkt_coupling for the many right-hand sides of NB=2 plans, so that the other solves' code is
+// unchanged; each value formed as the one-rhs pass forms it).
+template <class X, int NX, int NU, bool RB = false>
 BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdouble* r0, size_t rs, const gdouble* e0,
                         size_t es, gdouble* o0, size_t os, gdouble* n0, size_t ns, int ncw = 0) {
   const Ctx C = Cin.uniform();
@@ -2206,6 +2209,65 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   BMPC_TOC(C.ws, L, PROF_X3, t_fw);
   BMPC_TIC(t_post);
   // ---- post-pass: nu_k = -(l_k + P_k x_k), slack recovery -----------------------------------
+  if constexpr (RB) {   // four right-hand sides per pass: a node's P row, dh / Fx blend and slack weights loaded once
+    constexpr int NB4 = 4;
+    struct VR { double v[NB4]; };
+    for (int rb = 0; rb < nr; rb += NB4) {
+      const int rn = nr - rb < NB4 ? nr - rb : NB4;
+      if (n0) {
+        lane_batch<BMPC_TS_UN>(ex, 0, P.T * NX, [&](int it) {
+          const int k = it / NX, i = it % NX;
+          double pr[NX];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) pr[j] = ws[L.P + k * NX * NX + i * NX + j];
+          VR out;
+#pragma unroll
+          for (int a = 0; a < NB4; ++a) {
+            const int ri = rb + (a < rn ? a : 0);
+            const gdouble* o = o0 + ri * os;
+            double v = (ri >= ncw || needed(t.x_branch[k], ri)) ? lv_[ri * lstr + it] : 0.0;
+#pragma unroll
+            for (int j = 0; j < NX; ++j) v += pr[j] * o[P.oX + k * NX + j];
+            out.v[a] = -v;
+          }
+          return out;
+        }, [&](int it, const VR& r) {
+#pragma unroll
+          for (int a = 0; a < NB4; ++a)
+            if (a < rn) n0[(rb + a) * ns + it] = r.v[a];
+        });
+      }
+      lane_batch<BMPC_TS_UN>(ex, 0, P.T * Nc, [&](int it) {
+        const int k = it / Nc, c = it % Nc;
+        const double on = t.x_u[k] >= 0 ? 1.0 : 0.0;
+        double cf[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          const double dhv = dh[k * NX + j], fxj = fxv(P, ex, c > 0 ? c - 1 : 0, j), m0 = c == 0 ? 1.0 : 0.0;
+          cf[j] = m0 * (-dhv) + (1.0 - m0) * fxj;
+        }
+        const double s0 = sdv[it * 2], s1 = sdv[it * 2 + 1];
+        VR out;
+#pragma unroll
+        for (int a = 0; a < NB4; ++a) {
+          const int ri = rb + (a < rn ? a : 0);
+          const gdouble* o = o0 + ri * os;
+          double fx = 0.0;
+#pragma unroll
+          for (int j = 0; j < NX; ++j) fx += cf[j] * o[P.oX + k * NX + j];
+          out.v[a] = (r0[ri * rs + P.oS + it] + s1 * on * fx) / s0;
+        }
+        return out;
+      }, [&](int it, const VR& r) {
+#pragma unroll
+        for (int a = 0; a < NB4; ++a)
+          if (a < rn) o0[(rb + a) * os + P.oS + it] = r.v[a];
+      });
+    }
+    ex.sync();
+    BMPC_TOC(C.ws, L, PROF_X4, t_post);
+    return;
+  }
   for (int ri = 0; ri < nr; ++ri) {
     gdouble* o = o0 + ri * os;
     const gdouble* rr = r0 + ri * rs;
@@ -2381,8 +2443,12 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   BMPC_PROF(C.ws, L, PROF_COUPLING);
   gdouble* ws = C.ws;
   const int nc = P.ncones;
-  tree_solve<X, NX, NU>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv, ws + L.colnu,
-                        P.neq, nc);
+  if (ex.uniform(nc + extra >= 8))   // NB=2 plans (15 right-hand sides): the batched post-pass
+    tree_solve<X, NX, NU, true>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv,
+                                ws + L.colnu, P.neq, nc);
+  else
+    tree_solve<X, NX, NU>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv, ws + L.colnu,
+                          P.neq, nc);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
   auto* M = coup_mem(ex, ws, L, P, P.lds_M);
   const gdouble* eta = ws + L.eta;
