@@ -929,16 +929,27 @@ int bmpc_set_lane_ref(bmpc_plan* pl, int nref, const double* grid, const double*
   HIPCHECK(hipSetDevice(pl->ctx->device));
   HIPCHECK(hipStreamSynchronize(pl->stream));   // no solve in flight reads the old reference
   if (pl->user_stream) HIPCHECK(hipStreamSynchronize(pl->user_stream));
-  hipFree(pl->d_lref);
-  pl->d_lref = nullptr;
+  // the new copy is built beside the old one and swapped in only once the device bundle points
+  // at it: a failure on the way leaves the plan on its old, still allocated reference
+  DevBuf fresh;
   if (nref) {
-    HIPCHECK(hipMalloc(&pl->d_lref, sizeof(double) * 2 * (size_t)nref));
-    HIPCHECK(hipMemcpy(pl->d_lref, grid, sizeof(double) * nref, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(pl->d_lref + nref, values, sizeof(double) * nref, hipMemcpyHostToDevice));
+    HIPCHECK(fresh.alloc(sizeof(double) * 2 * (size_t)nref));
+    HIPCHECK(hipMemcpy(fresh.as<double>(), grid, sizeof(double) * nref, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(fresh.as<double>() + nref, values, sizeof(double) * nref, hipMemcpyHostToDevice));
   }
+  double* const old = pl->d_lref;
+  const int old_n = pl->hp.plan.nlref;
+  pl->d_lref = fresh.as<double>();
   pl->hp.plan.nlref = nref;
   pl->hp.plan.lref = nullptr;   // host copy unused; upload_bundle points the device copy at d_lref
-  HIPCHECK(upload_bundle(pl));
+  const hipError_t e = upload_bundle(pl);
+  if (e != hipSuccess) {
+    pl->d_lref = old;
+    pl->hp.plan.nlref = old_n;
+    return fail(-5, std::string("upload_bundle: ") + hipGetErrorString(e));
+  }
+  fresh.p = nullptr;   // owned by the plan now
+  hipFree(old);
   return 0;
 }
 

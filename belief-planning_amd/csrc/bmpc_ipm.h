@@ -2427,6 +2427,13 @@ BMPC_HD auto coup_mem(const X& ex, gdouble* ws, CLayout& L, CPlan& P, int off) {
 template <class X>
 BMPC_HD auto coup_vec(const X& ex, int off) { return ex.lds + off; }
 
+// right-hand sides from which the coupling tree solve takes the post-pass that loads a node's
+// data once per four right-hand sides (tree_solve<..., RB=true>); a separate instantiation
+// with the same arithmetic per right-hand side (tests/test_kernel_host.py compares the two)
+#ifndef BMPC_TS_POST_RB_MIN
+#define BMPC_TS_POST_RB_MIN 8
+#endif
+
 // global variable index -> position in the primal vector
 BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }
 
@@ -2443,7 +2450,7 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   BMPC_PROF(C.ws, L, PROF_COUPLING);
   gdouble* ws = C.ws;
   const int nc = P.ncones;
-  if (ex.uniform(nc + extra >= 8))   // NB=2 plans (15 right-hand sides): the batched post-pass
+  if (ex.uniform(nc + extra >= BMPC_TS_POST_RB_MIN))   // NB=2 plans (15 right-hand sides): the batched post-pass
     tree_solve<X, NX, NU, true>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv,
                                 ws + L.colnu, P.neq, nc);
   else

@@ -313,7 +313,8 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   // launch (bmpc_hip.hip, choose_lds_rich) keeps only the part before the coupling system and
   // finds the system in the slab (Layout::coup) -- deep trees, whose 50 x 50 system would
   // otherwise leave 7 egos per CU.
-  const int ncoup = P.nsm * P.nsm + 2 * P.nsm;
+  // (matrix, pivots and the two right-hand sides of a paired back half)
+  const int ncoup = P.nsm * P.nsm + 3 * P.nsm;
   // the first area holds W1 and Wu (filled at kernel start; the IPM's cone passes index their
   // rows per lane), at least the 64 doubles of the former reduction area
   P.lds_red = 0;
@@ -333,6 +334,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   P.lds_M = P.lds_rhs2 + P.nsm;
   P.nlds = P.lds_M + P.nsm * P.nsm;
   P.nlds_lean = P.lds_M;
+  if (P.nscr > 0 && P.nlds > 1248) return "internal: the tree-solve LDS staging overflows the 16-egos-per-CU budget";
 
   // ---- weights -----------------------------------------------------------------------------
   double Qm[BMPC_MAX_N * BMPC_MAX_N], Rm[BMPC_MAX_D * BMPC_MAX_D];

@@ -172,6 +172,48 @@ def launch_ranks(a):
     sys.exit(subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")))
 
 
+class _HostSimPlan:
+    """TEST-ONLY backend of this script (BMPC_BENCH_BACKEND=hostsim): the host build of the
+    kernel templates (tests/hostsim) behind the few BatchPlan calls the closed loop makes, on
+    CPU tensors, so that tests/test_bench_launch.py can drive bench.py's N > 1 path -- the
+    torchrun self-launch, sharding, the statistics all-reduce and max-over-ranks timing -- over
+    gloo without a GPU.  Its numbers are never a measurement: the JSON line names the backend."""
+
+    def __init__(self, desc, B):
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import hostsim_lib as H
+        self.hs = H.HostSim(desc, B)
+        self.T, self.U, self.bdim, self.nbranch = self.hs.T, self.hs.U, self.hs.bdim, self.hs.nbranch
+        self._ms = 0.0
+
+    def set_policies(self, rows):
+        self.hs.set_policies(rows)
+
+    def env_step(self, env, t, scene, up, tx, tz, tr, Jv, st, it, estats):
+        x, z, xref = self.hs.env_step(env, t, scene.numpy(), up.numpy(), Jv.numpy(), st.numpy(), it.numpy(),
+                                      estats.numpy())
+        tx.copy_(_torch().from_numpy(x)), tz.copy_(_torch().from_numpy(z)), tr.copy_(_torch().from_numpy(xref))
+
+    def solve(self, tx, tz, tr, up, Jv, st, it):
+        t0 = time.perf_counter()
+        r = self.hs.solve(tx.numpy(), tz.numpy(), tr.numpy())
+        self._ms += 1e3 * (time.perf_counter() - t0)
+        T = _torch()
+        up.copy_(T.from_numpy(r["upred"])), Jv.copy_(T.from_numpy(r["J"]))
+        st.copy_(T.from_numpy(r["status"])), it.copy_(T.from_numpy(r["iters"]))
+
+    def enable_timing(self, on=True):
+        self._ms = 0.0
+
+    def timing(self):
+        return dict(tree_ms=0.0, ipm_ms=self._ms)
+
+
+def _torch():
+    import torch
+    return torch
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); run directly with N > 1 it "
@@ -207,11 +249,22 @@ def main():
     rank, local, world = D.world()
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    D.init("nccl", device=dev)
+    host = os.environ.get("BMPC_BENCH_BACKEND") == "hostsim"   # test-only (see _HostSimPlan)
+    if host and quad:
+        raise SystemExit("bench.py: the hostsim test backend runs the highway workloads only")
+    if host:
+        dev = torch.device("cpu")
+        D.init("gloo")
+    else:   # the hardware-only lines of the N > 1 path: RCCL init with device_id, HIP streams
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        D.init("nccl", device=dev)
     if world > 1:
         assert dist.get_world_size() == world, (dist.get_world_size(), world)
+
+    def sync():
+        if not host:
+            torch.cuda.synchronize()
     # one global seeded population; rank r owns a contiguous shard of it
     G = a.global_batch or (a.batch or (1024 if quad else 4096)) * world
     lo, hi = D.shard(G, rank, world)
@@ -226,7 +279,7 @@ def main():
         desc = highway_desc(N=a.N, NB=a.NB)
         if robust:
             desc.controller = abi.CTRL_ROBUST
-        pl = plan.BatchPlan(desc, B, device=local)
+        pl = _HostSimPlan(desc, B) if host else plan.BatchPlan(desc, B, device=local)
         pl.set_policies(highway_policy_rows(tgt))
     tx = torch.tensor(x, device=dev, dtype=torch.float64)
     tz = torch.tensor(z, device=dev, dtype=torch.float64)
@@ -236,9 +289,10 @@ def main():
     st = torch.zeros(B, device=dev, dtype=torch.int32)
     it = torch.zeros(B, device=dev, dtype=torch.int32)
     # one dedicated stream: the library's kernels and torch's ops run in order on it
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sh = stream.cuda_stream
+    if not host:
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        sh = stream.cuda_stream
     env = abi.make_env()                       # main_branch.sim_overtake scene constants
     scene = torch.zeros((B, abi.ENV_STRIDE), device=dev, dtype=torch.float64)
     if not quad:
@@ -251,8 +305,11 @@ def main():
         """Highway_env.step around the solve, on the device (k_env): Euler steps with
         uPred[0], collision flag, obstacle backup argmax, lane bookkeeping / lane-change
         re-targeting, x_ref rule (Highway_env_branch.py:83-184, :421-429)."""
-        pl.env_step_device(env, tstep[0], scene.data_ptr(), up.data_ptr(), tx.data_ptr(), tz.data_ptr(),
-                           tr.data_ptr(), Jv.data_ptr(), st.data_ptr(), it.data_ptr(), estats.data_ptr(), sh)
+        if host:
+            pl.env_step(env, tstep[0], scene, up, tx, tz, tr, Jv, st, it, estats)
+        else:
+            pl.env_step_device(env, tstep[0], scene.data_ptr(), up.data_ptr(), tx.data_ptr(), tz.data_ptr(),
+                               tr.data_ptr(), Jv.data_ptr(), st.data_ptr(), it.data_ptr(), estats.data_ptr(), sh)
         tstep[0] += 1
 
     qdt, qv0 = 0.2, 0.2
@@ -285,14 +342,17 @@ def main():
         # one closed-loop step: scene update -> solve (inputs / outputs stay in HBM)
         if not quad:
             env_step()
-        pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
-                        Jv.data_ptr(), st.data_ptr(), it.data_ptr(), sh)
+        if host:
+            pl.solve(tx, tz, tr, up, Jv, st, it)
+        else:
+            pl.solve_device(tx.data_ptr(), tz.data_ptr(), tr.data_ptr(), up.data_ptr(), None, None,
+                            Jv.data_ptr(), st.data_ptr(), it.data_ptr(), sh)
         if quad:
             quad_env_step()
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     # per-kernel device timing over the timed steps themselves: HIP events recorded on the
     # launch stream around each kernel, read back after the region (no host synchronisation
     # inside it); the IPM iteration mean comes from the same launches
@@ -301,14 +361,14 @@ def main():
     estats.zero_()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
         it_sum.add_(it)
     stats = D.episode_stats(estats)
     D.reduce_stats(stats)        # the only collective: SUM, MAX for the flag
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
@@ -355,7 +415,8 @@ def main():
                                     f"highway robustMPC closed loop, N={a.N}, NB={a.NB}, m=3 " if robust else
                                     f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
                                    + f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
-                       "global_batch": G, "world_size": world, "parallelism": f"ego-sharded dp{world}"},
+                       "global_batch": G, "world_size": world, "parallelism": f"ego-sharded dp{world}",
+                       "shards": [list(D.shard(G, r, world)) for r in range(world)]},
             "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
                          "traffic": traffic, "traffic_source": tsrc, "traffic_key": key, "source_hash": src,
@@ -376,7 +437,9 @@ def main():
                             "any_collided": bool(st_h[D.STAT_ANY_COLLIDED] > 0),
                             "env": "device k_env (sim_overtake scene)" if not quad else "torch ops"},
         }
-        if not a.no_cpu_baseline and world == 1 and not (quad or robust):
+        if host:
+            out["backend"] = "hostsim (TEST-ONLY host build over gloo: not a measurement)"
+        if not a.no_cpu_baseline and world == 1 and not (quad or robust) and not host:
             cores, aff, quota = usable_cores()
             try:
                 cb = cpu_cxx_baseline(a.N, a.NB, min(a.cpu_egos, G), 3, cores)

@@ -160,3 +160,16 @@ def test_paired_solves_are_bit_identical():
         b = _seeded_closed_loop("-DBMPC_PAIR_BACK=0 -DBMPC_PAIR_REFINE=0", B, N, NB)
         for k in a:
             assert np.array_equal(a[k], b[k]), (N, NB, k)
+
+
+def test_batched_post_pass_is_bit_identical():
+    """The coupling tree solve of NB = 2 plans (15 right-hand sides) takes the post-pass that
+    loads a node's data once per four right-hand sides (tree_solve<..., RB=true>, from
+    BMPC_TS_POST_RB_MIN right-hand sides on).  Per right-hand side it forms every value as the
+    one-at-a-time post-pass does: a host build that never takes it gives the same bits."""
+    import numpy as np
+    for B, N, NB, steps in ((8, 8, 2, 2), (4, 30, 2, 1)):
+        a = _seeded_closed_loop("", B, N, NB, steps)
+        b = _seeded_closed_loop("-DBMPC_TS_POST_RB_MIN=1000", B, N, NB, steps)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (N, NB, k)

@@ -13,7 +13,7 @@ mkdir -p $out
 libof() { if [ "$1" = base ]; then echo $R/belief-planning_amd/libbmpc.so; else echo $R/belief-planning_amd/libbmpc_$1.so; fi; }
 for v in $VARS; do   # each variant's source hash (sidecar of the build), so a log names what it compared
   echo "variant $v: $(libof $v) source $(cat $(libof $v).srchash 2>/dev/null || echo unknown) md5 $(md5sum < $(libof $v) | cut -c1-12)"
-  BMPC_LIBRARY=$(libof $v) timeout -k 10 150 python tools/variant_check.py $out/vc_$v.npz ${QB%% *} || exit 1
+  BMPC_LIBRARY=$(libof $v) timeout -k 10 150 python tools/variant_check.py $out/vc_$v.npz $QB || exit 1   # same B N NB as the timed runs
 done
 OUT=$out VARS="$VARS" python - <<'PY'
 import os

@@ -22,10 +22,14 @@ def main():
     pl = plan.BatchPlan(highway_desc(N=N, NB=NB), B)
     pl.set_policies(highway_policy_rows(tgt))
     pl.enable_timing(True)
-    r = pl.solve(x, z, xref)
+    r0 = pl.solve(x, z, xref)
     c0 = pl.counters()
+    # the profiled solve is the same first solve tools/variant_check.py records (reset: no warm
+    # start carried over from the solve above), so its statuses compare with the product's
+    pl.reset()
     t0 = time.time()
     r = pl.solve(x, z, xref)
+    assert np.array_equal(r0["status"], r["status"]) and np.array_equal(r0["iters"], r["iters"])
     wall = time.time() - t0
     c = pl.counters() - c0
     tm = pl.timing()

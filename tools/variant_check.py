@@ -22,11 +22,13 @@ if os.environ.get("BMPC_OLD_ABI"):   # an older build: declare only the symbols 
 from bmpc.scenarios import highway_desc, highway_policy_rows, seeded_batch  # noqa: E402
 
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+N = int(sys.argv[3]) if len(sys.argv) > 3 else 20     # the plan the A/B times (tools/ab_pmc.sh QB_ARGS)
+NB = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 x, z, xref, tgt = seeded_batch(B, seed=0)
-pl = plan.BatchPlan(highway_desc(N=20, NB=1), B)
+pl = plan.BatchPlan(highway_desc(N=N, NB=NB), B)
 pl.set_policies(highway_policy_rows(tgt))
 r = pl.solve(x, z, xref)
 np.savez(sys.argv[1], status=r["status"], iters=r["iters"], J=r["J"], upred=r["upred"])
 st, cnt = np.unique(r["status"], return_counts=True)
-print(os.environ.get("BMPC_LIBRARY", "libbmpc.so"), "status", dict(zip(st.tolist(), cnt.tolist())),
+print(os.environ.get("BMPC_LIBRARY", "libbmpc.so"), f"B={B} N={N} NB={NB}", "status", dict(zip(st.tolist(), cnt.tolist())),
       "iters mean %.2f min %d" % (r["iters"].mean(), r["iters"].min()), flush=True)
