@@ -353,14 +353,59 @@ def unboost_dual(C, z, beta):
     return z
 
 
-def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL, verbose=False):
+EQUIL_ITERS = 3      # ECOS glblopts.h EQUIL_ITERS (RUIZ_EQUIL)
+EQUILIBRATE = False  # module default of ecos_solve(equilibrate=...)
+
+
+def equilibration(A, G, C, iters=EQUIL_ITERS):
+    """ECOS's Ruiz equilibration of [A; G] (ECOS 2.0.x ``equil.c``, ``use_ruiz_equilibration``,
+    run by ``ECOS_setup`` before the first iteration; restated, ECOS is not in this image):
+    ``iters`` rounds of -- column max-abs over A and G, row max-abs of A and of G, the rows of
+    each second-order cone given the SUM of their row maxima (one factor per cone keeps the cone
+    invariant), square roots (values below 1e-6 -> 1), rows and columns divided by them, the
+    factors accumulated.  Returns (xequil, Aequil, Gequil): the solver then works on
+    c / xequil, diag(1/Aequil) A diag(1/xequil), b / Aequil, diag(1/Gequil) G diag(1/xequil),
+    h / Gequil, and ``backscale`` returns x / xequil, y / Aequil, z / Gequil, s * Gequil."""
+    A = sp.csr_matrix(A, dtype=float, copy=True)
+    G = sp.csr_matrix(G, dtype=float, copy=True)
+    n = G.shape[1]
+    xe, ae, ge = np.ones(n), np.ones(A.shape[0]), np.ones(G.shape[0])
+
+    def rowmax(M):
+        return np.asarray(abs(M).max(axis=1).todense()).ravel() if M.shape[0] else np.zeros(0)
+
+    for _ in range(iters):
+        xt = np.asarray(abs(G).max(axis=0).todense()).ravel()
+        if A.shape[0]:
+            xt = np.maximum(xt, np.asarray(abs(A).max(axis=0).todense()).ravel())
+        at, gt = rowmax(A), rowmax(G)
+        for o, q in zip(C.off, C.q):
+            gt[o:o + q] = gt[o:o + q].sum()
+        xt, at, gt = (np.where(np.abs(v) < 1e-6, 1.0, np.sqrt(v)) for v in (xt, at, gt))
+        A = sp.diags(1.0 / at) @ A @ sp.diags(1.0 / xt)
+        G = sp.diags(1.0 / gt) @ G @ sp.diags(1.0 / xt)
+        xe, ae, ge = xe * xt, ae * at, ge * gt
+    return xe, ae, ge
+
+
+def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL, verbose=False, equilibrate=None):
     """Solve min c'x s.t. Ax = b, Gx + s = h, s in K. Returns (x, info).
 
-    ``prob.cone_boost`` (optional, per cone) applies :func:`boost_rows` first."""
+    ``equilibrate`` (default: module EQUILIBRATE) scales the data as ECOS_setup does
+    (:func:`equilibration`) and returns the back-scaled point; ``prob.cone_boost`` (optional,
+    per cone) then applies :func:`boost_rows` to the (scaled) cone rows."""
     C = Cones(prob.dims)
     beta = list(getattr(prob, 'cone_boost', None) or [0.0] * len(C.q))
-    G, h = boost_rows(C, prob.G.tocsc(), prob.h, beta)
     c, A, b = prob.c, prob.A.tocsc(), prob.b
+    G0, h0 = prob.G.tocsc(), prob.h
+    if EQUILIBRATE if equilibrate is None else equilibrate:
+        xe, ae, ge = equilibration(A, G0, C)
+        c, b, h0 = c / xe, b / ae, h0 / ge
+        A = (sp.diags(1.0 / ae) @ A @ sp.diags(1.0 / xe)).tocsc()
+        G0 = (sp.diags(1.0 / ge) @ G0 @ sp.diags(1.0 / xe)).tocsc()
+    else:
+        xe, ae, ge = np.ones(len(c)), np.ones(A.shape[0]), np.ones(G0.shape[0])
+    G, h = boost_rows(C, G0, h0, beta)
     n, p, m = G.shape[1], A.shape[0], G.shape[0]
     kkt = KKT(A, G, C)
     e = _unit(C)
@@ -381,9 +426,9 @@ def ecos_solve(prob, maxit=MAXIT, feastol=FEASTOL, abstol=ABSTOL, reltol=RELTOL,
 
     def pack(code, it, st, xs, ys, zs, ss, ts):
         info.update(st, exitFlag=code, iter=it)
-        info['x'], info['y'] = xs / ts, ys / ts
-        info['s'] = unboost_dual(C, ss / ts, [-v for v in beta])   # T^-1 = T_{-b}
-        info['z'] = unboost_dual(C, zs / ts, beta)
+        info['x'], info['y'] = xs / ts / xe, ys / ts / ae
+        info['s'] = unboost_dual(C, ss / ts, [-v for v in beta]) * ge   # T^-1 = T_{-b}
+        info['z'] = unboost_dual(C, zs / ts, beta) / ge
         return info['x'], info
 
     for it in range(maxit + 1):
