@@ -205,6 +205,9 @@ struct Layout {
   // IPM vectors
   size_t x, y, z, s, lam, x1, y1, z1, x2, y2, z2, dz, ds, rx, ry, rz, hvec, bvec;
   size_t ta, ta2, ya, ra, rb, rc, bestx;
+  // ECOS's equilibration of this solve (bmpc_ipm.h equilibrate): column factors (nv), A row factors
+  // (neq), G row factors (nrows; one value per second-order cone)
+  size_t xeq, aeq, geq;
   // KKT-solve scratch
   size_t k_r0, k_nv0, k_e1, k_e2, k_e3, k_t3, k_t3b, k_cx, k_cy, k_cz, k_nv1, zeros;
   // scaling

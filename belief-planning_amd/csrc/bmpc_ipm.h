@@ -18,6 +18,12 @@
 
 #include "bmpc_tree.h"
 
+#ifndef BMPC_EQUIL
+#define BMPC_EQUIL 1         // 0: no equilibration (the unscaled IPM of rounds 1-4)
+#endif
+#ifndef BMPC_EQUIL_ITERS
+#define BMPC_EQUIL_ITERS 3   // ECOS glblopts.h EQUIL_ITERS
+#endif
 #ifndef BMPC_PAIR_REFINE
 #define BMPC_PAIR_REFINE 1   // the pair's refinement rounds share their correction tree solves
 #endif
@@ -902,7 +908,8 @@ BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s
   return bad == 0.0;
 }
 
-// identity scaling for the initial point
+// identity scaling for the initial point: W = I of ECOS's equilibrated variables, i.e. W = diag(ge)
+// here (LP rows d = ge; a cone's eta = its ge, wbar = v = e0); ge = 1 without equilibration
 template <class X>
 BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   CPlan& P = *C.P;
@@ -910,14 +917,20 @@ BMPC_HD void identity_scaling(const X ex, const Ctx& C) {
   gdouble* wb = C.at(C.L->wbar);
   gdouble* vn = C.at(C.L->vnt);
   gdouble* dli = C.at(C.L->dli);
-  lane_batch(ex, 0, P.nlp, [&](int) { return 1.0; }, [&](int i, double v) { dl[i] = v; dli[i] = v; });
+  const gdouble* ge = C.at(C.L->geq);
+  struct DD { double d, di; };
+  lane_batch(ex, 0, P.nlp, [&](int i) {
+    const double g = BMPC_EQUIL ? ge[i] : 1.0;
+    return DD{g, 1.0 / g};
+  }, [&](int i, DD v) { dl[i] = v.d; dli[i] = v.di; });
   const int c0 = P.nlp;
   lane_batch(ex, c0, P.nrows, [&](int) { return 0.0; }, [&](int i, double v) { wb[i] = v; vn[i] = v; });
   ex.sync();
   for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
-    wb[topo_view(P, ex).cone_off[k]] = 1.0;
-    vn[topo_view(P, ex).cone_off[k]] = 1.0;
-    C.ws[C.L->eta + k] = 1.0;
+    const int off = topo_view(P, ex).cone_off[k];
+    wb[off] = 1.0;
+    vn[off] = 1.0;
+    C.ws[C.L->eta + k] = BMPC_EQUIL ? ge[off] : 1.0;
   }
   ex.sync();
 }
@@ -2996,6 +3009,205 @@ BMPC_HD double dot2(const X ex, const gdouble* a1, const gdouble* b1, int n1, co
   });
 }
 
+// ------------------------------------------------------------------------------------
+// ECOS's equilibration (ECOS_setup -> set_equilibration, ECOS 2.0.x equil.c with RUIZ_EQUIL and
+// EQUIL_ITERS = 3; restated in oracle/ecos_ipm.py:equilibration).  ECOS runs its IPM on
+//   c / xe,  diag(1/ae) A diag(1/xe),  b / ae,  diag(1/ge) G diag(1/xe),  h / ge
+// with xe, ae, ge the products over three rounds of sqrt(max-abs) of the current columns of
+// [A; G], rows of A and rows of G (the rows of a second-order cone share the SUM of their row
+// maxima; a maximum below 1e-6 gives 1).  The (unboosted) entries of A and G are enumerated
+// here from the structured operators (apply_A / apply_G and their transposes).
+//
+// The IPM itself stays in the unscaled variables: with x~ = xe x, y~ = ae y, z~ = ge z, s~ = s / ge
+// ECOS's Newton directions, step lengths and its NT scaling's lambda are those of the unscaled
+// problem (ge is one value per cone, so the cone scalings commute), so the equilibration only
+// enters where ECOS's iteration is not scale-invariant -- the initial point (W = I in the scaled
+// variables is W = ge here; bring2cone acts on the scaled vectors) and the norms of the exit
+// tests (ipm_solve below).
+// ------------------------------------------------------------------------------------
+
+template <class X, int NX, int NU>
+BMPC_FN void equilibrate(const X ex, const Ctx Cin) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  gdouble* xe = ws + L.xeq;
+  gdouble* ae = ws + L.aeq;
+  gdouble* ge = ws + L.geq;
+  gdouble* cm = ws + L.k_nv0;   // this round's column / row maxima (KKT scratch, free before the first solve)
+  gdouble* am = ws + L.k_e2;
+  gdouble* gm = ws + L.k_r0;
+  const auto t = topo_view(P, ex);
+  const int Nc = P.Nc, nv = P.nv, neq = P.neq, nr = P.nrows, T = P.T;
+  const gdouble* dh = ws + L.dh;
+  const gdouble* Ad = ws + L.Ad;
+  const gdouble* Bd = ws + L.Bd;
+  const gdouble* p = ws + L.p;
+  const double Qs = fabs(P.desc.Qslack[1]);
+  double qx[NX];
+  ctx_qx<NX>(C, qx);
+  for (int i = ex.lane; i < nv; i += ex.nlanes) xe[i] = 1.0;
+  for (int i = ex.lane; i < neq; i += ex.nlanes) ae[i] = 1.0;
+  for (int i = ex.lane; i < nr; i += ex.nlanes) ge[i] = 1.0;
+  ex.sync();
+  // coefficient of x_{k,j} in Fx row c of state node k (non-terminal k)
+  auto fcoef = [&](int k, int c, int j) { return c == 0 ? -dh[k * NX + j] : fxv(P, ex, c - 1, j); };
+  // cone k's first-row (F1) variables: cb / ci / c / has children (tail terms of apply_G)
+  for (int rnd = 0; rnd < BMPC_EQUIL_ITERS; ++rnd) {
+    // ---- G: LP rows -------------------------------------------------------------------------
+    for (int i = ex.lane; i < P.nlp; i += ex.nlanes) {
+      const double rf = ge[i];
+      double m = 0.0;
+      if (i >= P.rFx && i < P.rFx + T * Nc) {
+        const int it = i - P.rFx, k = it / Nc, c = it % Nc;
+        m = 1.0 / (rf * xe[P.oS + it]);
+        if (t.x_u[k] >= 0)
+          for (int j = 0; j < NX; ++j) m = fmax(m, fabs(fcoef(k, c, j)) / (rf * xe[P.oX + k * NX + j]));
+      } else if (i >= P.rPos && i < P.rPos + T * Nc) {
+        m = 1.0 / (rf * xe[P.oS + (i - P.rPos)]);
+      } else if (i >= P.rFu && i < P.rFu + P.U * P.nFu) {
+        const int it = i - P.rFu, u = it / P.nFu, r = it % P.nFu;
+        for (int j = 0; j < NU; ++j) m = fmax(m, fabs(fuv(P, ex, r, j)) / (rf * xe[P.oU + u * NU + j]));
+      } else {   // risk rows: -rho_b, then -mu+ / -mu-
+        const int it = i - P.rRisk;
+        m = 1.0 / (rf * xe[it < P.bdim ? P.oRho + it : P.oMup + (it - P.bdim)]);
+      }
+      gm[i] = m;
+    }
+    // ---- G: cone rows (one lane per cone: the rows' maxima summed over the cone) --------------
+    for (int k = ex.lane; k < P.ncones; k += ex.nlanes) {
+      const int off = t.cone_off[k], q = t.cone_q[k], c = t.cone_c[k];
+      const double rf = ge[off];   // one factor per cone
+      double f1 = 0.0, mid = 0.0;
+      if (c >= 0) {
+        const int ndx = t.br_ndx[c], ndu = t.br_ndu[c];
+        for (int j = 0; j < P.N; ++j) {
+          const int xk = ndx + j, uk = ndu + j;
+          for (int r = 0; r < NX; ++r) f1 = fmax(f1, 2.0 * fabs(qx[r]) / (rf * xe[P.oX + xk * NX + r]));
+          for (int cc = 0; cc < Nc; ++cc) f1 = fmax(f1, Qs / (rf * xe[P.oS + xk * Nc + cc]));
+          for (int rr = 0; rr < NX; ++rr) {
+            double m = 0.0;
+            for (int s2 = 0; s2 < NX; ++s2) m = fmax(m, 2.0 * fabs(w1v(P, ex, rr, s2)) / (rf * xe[P.oX + xk * NX + s2]));
+            mid += m;
+          }
+          for (int rr = 0; rr < NU; ++rr) {
+            double m = 0.0;
+            for (int s2 = 0; s2 < NU; ++s2) m = fmax(m, 2.0 * fabs(P.Wu[rr * NU + s2]) / (rf * xe[P.oU + uk * NU + s2]));
+            mid += m;
+          }
+        }
+        const int cb = t.cone_b[k], ci = t.cone_i[k];
+        f1 = fmax(f1, 1.0 / (rf * xe[P.oSig + cb]));
+        f1 = fmax(f1, 1.0 / (rf * xe[P.oMup + cb + ci]));
+        f1 = fmax(f1, 1.0 / (rf * xe[P.oMum + cb + ci]));
+        if (t.br_child0[c] >= 0) f1 = fmax(f1, 1.0 / (rf * xe[P.oRho + c]));
+      } else {   // the root cone: the root node's slacks, -J + rho_0, and the root input's Wu rows
+        for (int cc = 0; cc < Nc; ++cc) f1 = fmax(f1, Qs / (rf * xe[P.oS + cc]));
+        f1 = fmax(f1, 1.0 / (rf * xe[P.oJ]));
+        f1 = fmax(f1, 1.0 / (rf * xe[P.oRho]));
+        for (int rr = 0; rr < NU; ++rr) {
+          double m = 0.0;
+          for (int s2 = 0; s2 < NU; ++s2) m = fmax(m, 2.0 * fabs(P.Wu[rr * NU + s2]) / (rf * xe[P.oU + s2]));
+          mid += m;
+        }
+      }
+      const double tot = 2.0 * f1 + mid;   // first and last rows (+-F1) and the middle rows
+      for (int i = 0; i < q; ++i) gm[off + i] = tot;
+    }
+    // ---- A rows: dynamics, then the CVaR rows --------------------------------------------------
+    for (int i = ex.lane; i < neq; i += ex.nlanes) {
+      const double rf = ae[i];
+      double m = 0.0;
+      if (i < T * NX) {
+        const int k = i / NX, r = i % NX;
+        m = 1.0 / (rf * xe[P.oX + i]);
+        const int su = t.x_srcu[k], sx = t.x_srcx[k];
+        if (su >= 0) {
+          for (int s2 = 0; s2 < NX; ++s2) m = fmax(m, fabs(Ad[su * NX * NX + r * NX + s2]) / (rf * xe[P.oX + sx * NX + s2]));
+          for (int s2 = 0; s2 < NU; ++s2) m = fmax(m, fabs(Bd[su * NX * NU + r * NU + s2]) / (rf * xe[P.oU + su * NU + s2]));
+        }
+      } else {
+        const int b = i - T * NX;
+        m = fmax(1.0 / (rf * xe[P.oRho + b]), 1.0 / (rf * xe[P.oSig + b]));
+        for (int ii = 0; ii < P.m; ++ii)
+          m = fmax(m, fabs(p[b * P.m + ii] / P.desc.ralpha) / (rf * xe[P.oMum + b * P.m + ii]));
+      }
+      am[i] = m;
+    }
+    // ---- columns ---------------------------------------------------------------------------------
+    for (int col = ex.lane; col < nv; col += ex.nlanes) {
+      const double cf = xe[col];
+      double m = 0.0;
+      if (col >= P.oX && col < P.oX + T * NX) {
+        const int k = (col - P.oX) / NX, r = (col - P.oX) % NX;
+        if (t.x_u[k] >= 0)
+          for (int c = 0; c < Nc; ++c) m = fmax(m, fabs(fcoef(k, c, r)) / (ge[P.rFx + k * Nc + c] * cf));
+        const int kc = t.x_cone[k];
+        if (kc >= 0) {
+          const double rf = ge[t.cone_off[kc]];
+          m = fmax(m, 2.0 * fabs(qx[r]) / (rf * cf));
+          for (int rr = 0; rr < NX; ++rr) m = fmax(m, 2.0 * fabs(w1v(P, ex, rr, r)) / (rf * cf));
+        }
+        m = fmax(m, 1.0 / (ae[k * NX + r] * cf));
+        const int u = t.x_u[k];
+        if (u >= 0)
+          for (int e = t.succ_off[k]; e < t.succ_off[k + 1]; ++e) {
+            const int kn = t.succ[e];
+            for (int rr = 0; rr < NX; ++rr) m = fmax(m, fabs(Ad[u * NX * NX + rr * NX + r]) / (ae[kn * NX + rr] * cf));
+          }
+      } else if (col >= P.oU && col < P.oU + P.U * NU) {
+        const int u = (col - P.oU) / NU, s2 = (col - P.oU) % NU;
+        for (int r = 0; r < P.nFu; ++r) m = fmax(m, fabs(fuv(P, ex, r, s2)) / (ge[P.rFu + u * P.nFu + r] * cf));
+        const int kc = t.u_cone[u];
+        if (kc >= 0) {
+          const double rf = ge[t.cone_off[kc]];
+          for (int rr = 0; rr < NU; ++rr) m = fmax(m, 2.0 * fabs(P.Wu[rr * NU + s2]) / (rf * cf));
+        }
+        const int k = t.u_x[u];
+        for (int e = t.succ_off[k]; e < t.succ_off[k + 1]; ++e) {
+          const int kn = t.succ[e];
+          for (int rr = 0; rr < NX; ++rr) m = fmax(m, fabs(Bd[u * NX * NU + rr * NU + s2]) / (ae[kn * NX + rr] * cf));
+        }
+      } else if (col >= P.oS && col < P.oS + T * Nc) {
+        const int it = col - P.oS, k = it / Nc;
+        m = fmax(1.0 / (ge[P.rFx + it] * cf), 1.0 / (ge[P.rPos + it] * cf));
+        const int kc = t.x_cone[k] >= 0 ? t.x_cone[k] : (k == 0 ? P.ncones - 1 : -1);
+        if (kc >= 0) m = fmax(m, Qs / (ge[t.cone_off[kc]] * cf));
+      } else {   // the globals: risk row, the cones' first rows, the CVaR equality rows
+        if (col < P.oSig) m = 1.0 / (ge[P.rRisk + (col - P.oRho)] * cf);
+        else if (col >= P.oMup && col < P.oS) m = 1.0 / (ge[P.rRisk + P.bdim + (col - P.oMup)] * cf);
+        for (int k = 0; k < P.ncones; ++k) {
+          const int c = t.cone_c[k];
+          bool on = false;
+          if (c >= 0) {
+            const int b = t.cone_b[k], ii = t.cone_i[k];
+            on = col == P.oSig + b || col == P.oMup + b + ii || col == P.oMum + b + ii ||
+                 (t.br_child0[c] >= 0 && col == P.oRho + c);
+          } else {
+            on = col == P.oJ || col == P.oRho;
+          }
+          if (on) m = fmax(m, 1.0 / (ge[t.cone_off[k]] * cf));
+        }
+        if (col < P.oMup) {   // rho_b, sigma_b: +1 in CVaR row b
+          const int b = col < P.oSig ? col - P.oRho : col - P.oSig;
+          m = fmax(m, 1.0 / (ae[T * NX + b] * cf));
+        } else if (col >= P.oMum && col < P.oS) {
+          const int j = col - P.oMum;
+          m = fmax(m, fabs(p[j] / P.desc.ralpha) / (ae[T * NX + j / P.m] * cf));
+        }
+      }
+      cm[col] = m;
+    }
+    ex.sync();
+    auto fac = [](double v) { return fabs(v) < 1e-6 ? 1.0 : sqrt(v); };
+    for (int i = ex.lane; i < nv; i += ex.nlanes) xe[i] *= fac(cm[i]);
+    for (int i = ex.lane; i < neq; i += ex.nlanes) ae[i] *= fac(am[i]);
+    for (int i = ex.lane; i < nr; i += ex.nlanes) ge[i] *= fac(gm[i]);
+    ex.sync();
+  }
+}
+
 struct IpmResult {
   int exit_flag;
   int iters;
@@ -3041,8 +3253,15 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   BMPC_PROF(ws, L, PROF_TOTAL);
   BMPC_TIC(t_init);
 
+  // ECOS's equilibration factors (all 1 without it): the exit tests' norms are those of the
+  // equilibrated residuals and iterates -- ||r_x / xe||, ||r_y / ae||, ||r_z / ge||, ||xe x||, ||ae y||,
+  // ||ge z||, ||s / ge|| -- and the initial point is ECOS's in the equilibrated variables
+  const gdouble* xq = ws + L.xeq;
+  const gdouble* aq = ws + L.aeq;
+  const gdouble* gq = ws + L.geq;
+  if (BMPC_EQUIL) equilibrate<X, NX, NU>(ex, C);
   build_hb<X, NX, NU>(ex, C, hv, bv);
-  // ---- initial point with W = I ----------------------------------------------------------
+  // ---- initial point with W = I (of the equilibrated variables) ----------------------------
   identity_scaling(ex, C);
   if (!kkt_factor<X, NX, NU>(ex, C, true) || !kkt_coupling<X, NX, NU>(ex, C, 0)) {
     res.exit_flag = EXIT_NUMERICS;
@@ -3051,19 +3270,40 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
   lane_batch<16>(ex, 0, nv, [&](int i) { return 0.0; }, [&](int i, double v) { tA[i] = v; });
   ex.sync();
   kkt_solve<X, NX, NU>(ex, C, tA, bv, hv, x, y2, z2, BMPC_NITREF_INIT);
-  lane_batch<16>(ex, 0, nr, [&](int i) { return -z2[i]; }, [&](int i, double v) { ra[i] = v; });
+  // s = ge bring2cone(-ge z)  (ECOS: s~ = bring2cone(-z~), z~ = ge z, s = ge s~)
+  lane_batch<16>(ex, 0, nr, [&](int i) { return -(BMPC_EQUIL ? gq[i] : 1.0) * z2[i]; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
   bring2cone(ex, C, ra, s);
+  if (BMPC_EQUIL) {
+    lane_batch<16>(ex, 0, nr, [&](int i) { return gq[i] * s[i]; }, [&](int i, double v) { s[i] = v; });
+    ex.sync();
+  }
   lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
   lane_batch(ex, 0, neq, [&](int i) { return 0.0; }, [&](int i, double v) { ya[i] = v; });
   lane_batch<16>(ex, 0, nr, [&](int i) { return 0.0; }, [&](int i, double v) { ra[i] = v; });
   ex.sync();
   kkt_solve<X, NX, NU>(ex, C, tA, ya, ra, x2, y, z2, BMPC_NITREF_INIT);
+  // z = bring2cone(ge z) / ge
+  if (BMPC_EQUIL) {
+    lane_batch<16>(ex, 0, nr, [&](int i) { return gq[i] * z2[i]; }, [&](int i, double v) { z2[i] = v; });
+    ex.sync();
+  }
   bring2cone(ex, C, z2, z);
+  if (BMPC_EQUIL) {
+    lane_batch<16>(ex, 0, nr, [&](int i) { return z[i] / gq[i]; }, [&](int i, double v) { z[i] = v; });
+    ex.sync();
+  }
   double tau = 1.0, kap = 1.0;
-  const double resx0 = 1.0;   // max(1, ||c||), c = e_J
-  const double resy0 = fmax(1.0, sqrt(vdot(ex, bv, bv, neq)));
-  const double resz0 = fmax(1.0, sqrt(vdot(ex, hv, hv, nr)));
+  // max(1, ||c~||), c~ = e_J / xe_J;  max(1, ||b / ae||);  max(1, ||h / ge||)
+  const double resx0 = BMPC_EQUIL ? fmax(1.0, 1.0 / xq[P.oJ]) : 1.0;
+  const double resy0 = fmax(1.0, sqrt(lane_sum(ex, 0, neq, [&](int i) {
+    const double v = BMPC_EQUIL ? bv[i] / aq[i] : bv[i];
+    return v * v;
+  })));
+  const double resz0 = fmax(1.0, sqrt(lane_sum(ex, 0, nr, [&](int i) {
+    const double v = BMPC_EQUIL ? hv[i] / gq[i] : hv[i];
+    return v * v;
+  })));
   double best_score = 1e300, best_tau = 1.0;
   int best_it = 0;
   BMPC_TOC(ws, L, PROF_INIT, t_init);
@@ -3084,24 +3324,28 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     apply_AT<X, NX, NU>(ex, C, y, rx);
     apply_GT<X, NX, NU>(ex, C, z, tA);
     // the norms and dot products are accumulated in the passes that produce rx, ry, rz
-    struct R2 { double v, a; };
-    struct R3 { double v, a, b; };
-    struct R5 { double v, a, b, c, d; };
     double acx[2] = {0.0, 0.0}, acy[3] = {0.0, 0.0, 0.0}, acz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    // each pass also forms its residual's and iterate's equilibrated norms (r / xe, xe x, ...)
+    struct R2b { double v, rs, xs; };
     lane_batch<8>(ex, 0, nv, [&](int i) {
-      const double xi = x[i];
-      return R2{rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0)), xi * xi};
-    }, [&](int i, R2 r) { rx[i] = r.v; acx[0] += r.v * r.v; acx[1] += r.a; });
+      const double xi = x[i], q = BMPC_EQUIL ? xq[i] : 1.0;
+      const double v = rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0));
+      return R2b{v, v / q, q * xi};
+    }, [&](int i, R2b r) { rx[i] = r.v; acx[0] += r.rs * r.rs; acx[1] += r.xs * r.xs; });
     apply_A<X, NX, NU>(ex, C, x, ry);
+    struct R4 { double v, rs, a, ys; };
     lane_batch<8>(ex, 0, neq, [&](int i) {
-      const double yi = y[i], bi = bv[i];
-      return R3{bi * tau - ry[i], bi * yi, yi * yi};
-    }, [&](int i, R3 r) { ry[i] = r.v; acy[0] += r.v * r.v; acy[1] += r.a; acy[2] += r.b; });
+      const double yi = y[i], bi = bv[i], q = BMPC_EQUIL ? aq[i] : 1.0;
+      const double v = bi * tau - ry[i];
+      return R4{v, v / q, bi * yi, q * yi};
+    }, [&](int i, R4 r) { ry[i] = r.v; acy[0] += r.rs * r.rs; acy[1] += r.a; acy[2] += r.ys * r.ys; });
     apply_G<X, NX, NU>(ex, C, x, rz);
+    struct R7 { double v, rs, a, zs, ss, sz; };
     lane_batch<4>(ex, 0, nr, [&](int i) {
-      const double zi = z[i], si = s[i], hi = hv[i];
-      return R5{hi * tau - rz[i] - si, hi * zi, zi * zi, si * si, si * zi};
-    }, [&](int i, R5 r) { rz[i] = r.v; acz[0] += r.v * r.v; acz[1] += r.a; acz[2] += r.b; acz[3] += r.c; acz[4] += r.d; });
+      const double zi = z[i], si = s[i], hi = hv[i], q = BMPC_EQUIL ? gq[i] : 1.0;
+      const double v = hi * tau - rz[i] - si;
+      return R7{v, v / q, hi * zi, q * zi, si / q, si * zi};
+    }, [&](int i, R7 r) { rz[i] = r.v; acz[0] += r.rs * r.rs; acz[1] += r.a; acz[2] += r.zs * r.zs; acz[3] += r.ss * r.ss; acz[4] += r.sz; });
     ex.sync();
     const double cx = x[P.oJ];
     // the ten sums in one reduction (one barrier pair on a multi-wave executor)
@@ -3126,15 +3370,20 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
     // infeasibility certificates (only evaluated when their preconditions hold)
     double pinfres = -1.0, dinfres = -1.0;
     if ((hz + by) / fmax(ny + nz, 1.0) < -reltol) {
-      lane_batch<16>(ex, 0, nv, [&](int i) { return rx[i] - (i == P.oJ ? tau : 0.0); }, [&](int i, double v) { ra[i] = v; });
+      lane_batch<16>(ex, 0, nv, [&](int i) { return (rx[i] - (i == P.oJ ? tau : 0.0)) / (BMPC_EQUIL ? xq[i] : 1.0); },
+                     [&](int i, double v) { ra[i] = v; });
       ex.sync();
       pinfres = sqrt(vdot(ex, ra, ra, nv)) / fmax(ny + nz, 1.0);
     }
     if (cx / fmax(nx, 1.0) < -reltol) {
       apply_A<X, NX, NU>(ex, C, x, rb);
-      const double a1 = sqrt(vdot(ex, rb, rb, neq)) / fmax(nx, 1.0);
+      const double a1 = sqrt(lane_sum(ex, 0, neq, [&](int i) {
+        const double v = rb[i] / (BMPC_EQUIL ? aq[i] : 1.0);
+        return v * v;
+      })) / fmax(nx, 1.0);
       apply_G<X, NX, NU>(ex, C, x, ra);
-      lane_batch<16>(ex, 0, nr, [&](int i) { return ra[i] + (s[i]); }, [&](int i, double v) { ra[i] = v; });
+      lane_batch<16>(ex, 0, nr, [&](int i) { return (ra[i] + s[i]) / (BMPC_EQUIL ? gq[i] : 1.0); },
+                     [&](int i, double v) { ra[i] = v; });
       ex.sync();
       const double a2 = sqrt(vdot(ex, ra, ra, nr)) / fmax(nx + ns, 1.0);
       dinfres = fmax(a1, a2);

@@ -414,6 +414,9 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.rb = take(nr);
   L.rc = take(nr);
   L.bestx = take(nv);
+  L.xeq = take(nv);
+  L.aeq = take(neq);
+  L.geq = take(nr);
   L.k_r0 = take(nr);
   L.k_nv0 = take(nv);
   L.k_e1 = take(2 * (size_t)nv);    // two halves: the pair's refinement (kkt_refine_pair)

@@ -77,6 +77,7 @@ BMPC_HD void ph_init1(const X ex, const Ctx& C) {
   CLayout& L = *C.L;
   gdouble* ws = C.ws;
   gdouble* st = ws + L.ist;
+  if (BMPC_EQUIL) equilibrate<X, NX, NU>(ex, C);   // (ipm_solve: the same initial point and norms)
   build_hb<X, NX, NU>(ex, C, ws + L.hvec, ws + L.bvec);
   identity_scaling(ex, C);
   const bool ok = ex.uniform(kkt_factor<X, NX, NU>(ex, C, true));
@@ -131,14 +132,31 @@ BMPC_HD void ph_init3(const X ex, const Ctx& C) {
     gdouble* dx = uniform_ptr(ws + (p0 ? L.x : L.x2));
     gdouble* dy = uniform_ptr(ws + (p0 ? L.y2 : L.y));
     kkt_solve<X, NX, NU>(ex, C, tA, r2, r3, dx, dy, z2, BMPC_NITREF_INIT);
+    const gdouble* gq = ws + L.geq;
     if (p0) {
-      lane_batch<16>(ex, 0, nr, [&](int i) { return -z2[i]; }, [&](int i, double v) { ra[i] = v; });
+      lane_batch<16>(ex, 0, nr, [&](int i) { return -(BMPC_EQUIL ? gq[i] : 1.0) * z2[i]; }, [&](int i, double v) { ra[i] = v; });
+      ex.sync();
+    } else if (BMPC_EQUIL) {
+      lane_batch<16>(ex, 0, nr, [&](int i) { return gq[i] * z2[i]; }, [&](int i, double v) { z2[i] = v; });
       ex.sync();
     }
-    bring2cone(ex, C, uniform_ptr(p0 ? (const gdouble*)ra : (const gdouble*)z2), uniform_ptr(ws + (p0 ? L.s : L.z)));
+    gdouble* sz = uniform_ptr(ws + (p0 ? L.s : L.z));
+    bring2cone(ex, C, uniform_ptr(p0 ? (const gdouble*)ra : (const gdouble*)z2), sz);
+    if (BMPC_EQUIL) {   // s = ge s~, z = z~ / ge
+      lane_batch<16>(ex, 0, nr, [&](int i) { return p0 ? gq[i] * sz[i] : sz[i] / gq[i]; }, [&](int i, double v) { sz[i] = v; });
+      ex.sync();
+    }
   }
-  const double resy0 = fmax(1.0, sqrt(vdot(ex, bv, bv, neq)));
-  const double resz0 = fmax(1.0, sqrt(vdot(ex, hv, hv, nr)));
+  const gdouble* aq = ws + L.aeq;
+  const gdouble* gq = ws + L.geq;
+  const double resy0 = fmax(1.0, sqrt(lane_sum(ex, 0, neq, [&](int i) {
+    const double v = BMPC_EQUIL ? bv[i] / aq[i] : bv[i];
+    return v * v;
+  })));
+  const double resz0 = fmax(1.0, sqrt(lane_sum(ex, 0, nr, [&](int i) {
+    const double v = BMPC_EQUIL ? hv[i] / gq[i] : hv[i];
+    return v * v;
+  })));
   if (ex.lane == 0) {
     st[IS_ACTIVE] = 1.0;
     st[IS_TAU] = 1.0;
@@ -175,29 +193,36 @@ BMPC_HD void ph_res(const X ex, const Ctx& C, int it) {
   const double feastol = P.desc.feastol, abstol = P.desc.abstol, reltol = P.desc.reltol;
   const double deg = (double)(P.nlp + P.ncones);
   const double tau = st[IS_TAU], kap = st[IS_KAP];
-  const double resx0 = 1.0, resy0 = st[IS_RESY0], resz0 = st[IS_RESZ0];
+  const gdouble* xq = ws + L.xeq;
+  const gdouble* aq = ws + L.aeq;
+  const gdouble* gq = ws + L.geq;
+  const double resx0 = BMPC_EQUIL ? fmax(1.0, 1.0 / xq[P.oJ]) : 1.0, resy0 = st[IS_RESY0], resz0 = st[IS_RESZ0];
   double best_score = st[IS_BEST];
 
   apply_AT<X, NX, NU>(ex, C, y, rx);
   apply_GT<X, NX, NU>(ex, C, z, tA);
-  struct R2 { double v, a; };
-  struct R3 { double v, a, b; };
-  struct R5 { double v, a, b, c, d; };
+  // (ipm_solve's passes: the equilibrated norms formed with the residuals)
   double acx[2] = {0.0, 0.0}, acy[3] = {0.0, 0.0, 0.0}, acz[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  struct R2b { double v, rs, xs; };
   lane_batch<8>(ex, 0, nv, [&](int i) {
-    const double xi = x[i];
-    return R2{rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0)), xi * xi};
-  }, [&](int i, R2 r) { rx[i] = r.v; acx[0] += r.v * r.v; acx[1] += r.a; });
+    const double xi = x[i], q = BMPC_EQUIL ? xq[i] : 1.0;
+    const double v = rx[i] + (tA[i] + (i == P.oJ ? tau : 0.0));
+    return R2b{v, v / q, q * xi};
+  }, [&](int i, R2b r) { rx[i] = r.v; acx[0] += r.rs * r.rs; acx[1] += r.xs * r.xs; });
   apply_A<X, NX, NU>(ex, C, x, ry);
+  struct R4 { double v, rs, a, ys; };
   lane_batch<8>(ex, 0, neq, [&](int i) {
-    const double yi = y[i], bi = bv[i];
-    return R3{bi * tau - ry[i], bi * yi, yi * yi};
-  }, [&](int i, R3 r) { ry[i] = r.v; acy[0] += r.v * r.v; acy[1] += r.a; acy[2] += r.b; });
+    const double yi = y[i], bi = bv[i], q = BMPC_EQUIL ? aq[i] : 1.0;
+    const double v = bi * tau - ry[i];
+    return R4{v, v / q, bi * yi, q * yi};
+  }, [&](int i, R4 r) { ry[i] = r.v; acy[0] += r.rs * r.rs; acy[1] += r.a; acy[2] += r.ys * r.ys; });
   apply_G<X, NX, NU>(ex, C, x, rz);
+  struct R7 { double v, rs, a, zs, ss, sz; };
   lane_batch<4>(ex, 0, nr, [&](int i) {
-    const double zi = z[i], si = s[i], hi = hv[i];
-    return R5{hi * tau - rz[i] - si, hi * zi, zi * zi, si * si, si * zi};
-  }, [&](int i, R5 r) { rz[i] = r.v; acz[0] += r.v * r.v; acz[1] += r.a; acz[2] += r.b; acz[3] += r.c; acz[4] += r.d; });
+    const double zi = z[i], si = s[i], hi = hv[i], q = BMPC_EQUIL ? gq[i] : 1.0;
+    const double v = hi * tau - rz[i] - si;
+    return R7{v, v / q, hi * zi, q * zi, si / q, si * zi};
+  }, [&](int i, R7 r) { rz[i] = r.v; acz[0] += r.rs * r.rs; acz[1] += r.a; acz[2] += r.zs * r.zs; acz[3] += r.ss * r.ss; acz[4] += r.sz; });
   ex.sync();
   const double cx = x[P.oJ];
   const double by = ex.sum(acy[1]), hz = ex.sum(acz[1]);
@@ -217,15 +242,20 @@ BMPC_HD void ph_res(const X ex, const Ctx& C, int it) {
   const double dres = sqrt(ex.sum(acx[0])) / fmax(resx0 + ny + nz, 1.0) / tau;
   double pinfres = -1.0, dinfres = -1.0;
   if (ex.uniform((hz + by) / fmax(ny + nz, 1.0) < -reltol)) {
-    lane_batch<16>(ex, 0, nv, [&](int i) { return rx[i] - (i == P.oJ ? tau : 0.0); }, [&](int i, double v) { ra[i] = v; });
+    lane_batch<16>(ex, 0, nv, [&](int i) { return (rx[i] - (i == P.oJ ? tau : 0.0)) / (BMPC_EQUIL ? xq[i] : 1.0); },
+                   [&](int i, double v) { ra[i] = v; });
     ex.sync();
     pinfres = sqrt(vdot(ex, ra, ra, nv)) / fmax(ny + nz, 1.0);
   }
   if (ex.uniform(cx / fmax(nx, 1.0) < -reltol)) {
     apply_A<X, NX, NU>(ex, C, x, rb);
-    const double a1 = sqrt(vdot(ex, rb, rb, neq)) / fmax(nx, 1.0);
+    const double a1 = sqrt(lane_sum(ex, 0, neq, [&](int i) {
+      const double v = rb[i] / (BMPC_EQUIL ? aq[i] : 1.0);
+      return v * v;
+    })) / fmax(nx, 1.0);
     apply_G<X, NX, NU>(ex, C, x, ra);
-    lane_batch<16>(ex, 0, nr, [&](int i) { return ra[i] + (s[i]); }, [&](int i, double v) { ra[i] = v; });
+    lane_batch<16>(ex, 0, nr, [&](int i) { return (ra[i] + s[i]) / (BMPC_EQUIL ? gq[i] : 1.0); },
+                   [&](int i, double v) { ra[i] = v; });
     ex.sync();
     const double a2 = sqrt(vdot(ex, ra, ra, nr)) / fmax(nx + ns, 1.0);
     dinfres = fmax(a1, a2);

@@ -354,7 +354,7 @@ def unboost_dual(C, z, beta):
 
 
 EQUIL_ITERS = 3      # ECOS glblopts.h EQUIL_ITERS (RUIZ_EQUIL)
-EQUILIBRATE = False  # module default of ecos_solve(equilibrate=...)
+EQUILIBRATE = True   # module default of ecos_solve(equilibrate=...): ECOS equilibrates (ECOS_setup)
 
 
 def equilibration(A, G, C, iters=EQUIL_ITERS):

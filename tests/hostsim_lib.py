@@ -169,7 +169,7 @@ class HostSim:
         src = open(os.path.join(PKG, "csrc", "bmpc_core.h")).read()
         body = src[src.index("struct Layout {"):src.index("};", src.index("struct Layout {"))]
         names = [n for line in body.splitlines() if line.strip().startswith("size_t")
-                 for n in re.findall(r"(\w+)\s*[,;]", line.split("size_t", 1)[1])]
+                 for n in re.findall(r"(\w+)\s*[,;]", line.split("//", 1)[0].split("size_t", 1)[1])]
         out = np.zeros(256, np.uint64)
         cnt = lib().hs_layout(self.h, _p(out))
         assert cnt == len(names), (cnt, names)

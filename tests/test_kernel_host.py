@@ -8,8 +8,9 @@ relative and uPred[0] to 1e-6 absolute (observed at most 4.7e-7, on
 the N=30 NB=2 loop, and <= 6e-8 on the others); exit 10 ("inaccurate", ECOS stopped at 1e-4/5e-5)
 steps to 1e-4 relative / 5e-3 absolute -- those optima are only defined that loosely.
 Whether a step ends 0 or 10 is decided at the rounding floor, so exit codes must agree on
-at least 90% of the steps (observed: all 20 of highway_n10_nb1, 92 of 100 of n20_nb1, all 40
-of n8_nb2).  The solver exits by ECOS's rules only -- full accuracy, or reduced accuracy of
+at least 95% of the steps (observed with ECOS's equilibration in the oracle and the kernel,
+round 5: all 20 of highway_n10_nb1, 99 of 100 of n20_nb1, all 40 of n8_nb2; rounds 1-4,
+unequilibrated: 92 of 100 on n20_nb1).  The solver exits by ECOS's rules only -- full accuracy, or reduced accuracy of
 the best iterate at maxit / on a failed step; the earlier 5-iteration stall exit is gone (it
 never fired on these scenes nor on a 512-ego seeded batch).
 """
@@ -27,7 +28,7 @@ def check_replay(r, g, T, tree=None):
     u = np.asarray(g["traj_u"][:T])
     assert np.all(r["status"] >= 0), r["status"]
     # ECOS exit 0 vs 10 is decided at the 1e-8 rounding floor; most steps must agree exactly
-    assert np.mean(r["status"] == exits) >= 0.9, (r["status"], exits)
+    assert np.mean(r["status"] == exits) >= 0.95, (r["status"], exits)
     for t in range(T):
         tight = exits[t] == 0 and r["status"][t] == 0
         rtol, atol = (1e-6, 1e-6) if tight else (1e-4, 5e-3)

@@ -42,27 +42,23 @@ def replay_inputs(g, steps=None):
 
 
 def check_merge_replay(r, g, T):
-    """Exit codes agree on >= 90% of the steps.  Tolerances: J to 1e-6 relative (exit 0);
-    uPred[0] to 5e-4.  The merge cost is
-    ~3e4, so ECOS's 1e-8 relative gap fixes J to ~3e-4 absolute, and through the input cost
-    (R = diag(1, 100)) that only pins u to ~1e-2; late in the scene (u ~ 1e-2) the recorded
-    and the kernel's optima differ by up to ~1.2e-4 in the acceleration."""
+    """Exit codes agree on >= 95% of the steps (57 of 60).  Tolerances on exit-0 steps: J to
+    1e-6 relative, uPred[0] to 1e-5 (observed: 1.8e-6 on the host build); exit-10 steps 1e-4 /
+    5e-3.
+
+    With ECOS's equilibration in the oracle and the kernel (bmpc_ipm.h equilibrate; round 5) the
+    recorded scene exits 0 on all 60 steps and the host build agrees on all 60.  Without it
+    (rounds 1-4) the ~3e4 merge cost put ECOS's 1e-8 relative gap at the precision floor of the
+    unscaled problem: 5 of the recorded steps exited 10, the host build agreed on 54 of 60 and
+    uPred[0] was held to 5e-4."""
     exits, J, u = (np.asarray(g[k][:T]) for k in ("traj_exit", "traj_J", "traj_u"))
     assert np.all(r["status"] >= 0), r["status"]
-    # exit 0 vs 10 at the rounding floor: the merge cost (~3e4) puts ECOS's 1e-8 relative gap at
-    # the precision floor of the structured KKT solve.  Traced on the host build's step 33 (it
-    # exits 10 where the recording exits 0): at iteration 20 pres 3.4e-10, dres 1.2e-10 but the
-    # relative gap is 1.55e-8 (> 1e-8); the next step meets the gap (2.3e-10) and lifts pres to
-    # 2.4e-8 (> 1e-8), the one after to 4.8e-5, the step then fails and ECOS backtracks to the
-    # best iterate (exit 10) -- the KKT solves refine to ~1e-15 of their scale throughout.  Host
-    # build 54 of 60 agree, GPU 57 of 60 (profiles/r03/r03w_gpu_tests.log): the highway scenes'
-    # 90% bar holds here too
     agree = float(np.mean(r["status"] == exits))
     print(f"merge replay: exit codes agree on {agree:.3f} of {T} steps")
-    assert agree >= 0.9, (r["status"], exits)
+    assert agree >= 0.95, (r["status"], exits)
     for t in range(T):
         tight = exits[t] == 0 and r["status"][t] == 0
-        rtol, atol = (1e-6, 5e-4) if tight else (1e-4, 5e-3)
+        rtol, atol = (1e-6, 1e-5) if tight else (1e-4, 5e-3)
         assert abs(r["J"][t] - J[t]) <= rtol * max(1.0, abs(J[t])), (t, exits[t], r["J"][t], J[t])
         np.testing.assert_allclose(r["upred"][t, 0], u[t], atol=atol, err_msg=f"step {t}")
 
