@@ -24,6 +24,15 @@
 #ifndef BMPC_EQUIL_ITERS
 #define BMPC_EQUIL_ITERS 3   // ECOS glblopts.h EQUIL_ITERS
 #endif
+// right-hand sides from which the coupling tree solve takes the post-pass that loads a node's
+// data once per four right-hand sides (tree_solve<..., RB=true>); a separate instantiation
+// with the same arithmetic per right-hand side (tests/test_kernel_host.py compares the two)
+#ifndef BMPC_TS_POST_RB_MIN
+#define BMPC_TS_POST_RB_MIN 8
+#endif
+#ifndef BMPC_TS_POST_RB
+#define BMPC_TS_POST_RB 4    // right-hand sides per pass of that post-pass
+#endif
 #ifndef BMPC_PAIR_REFINE
 #define BMPC_PAIR_REFINE 1   // the pair's refinement rounds share their correction tree solves
 #endif
@@ -2222,8 +2231,8 @@ BMPC_FN_TREE_SOLVE void tree_solve(const X ex, const Ctx Cin, int nr, const gdou
   BMPC_TOC(C.ws, L, PROF_X3, t_fw);
   BMPC_TIC(t_post);
   // ---- post-pass: nu_k = -(l_k + P_k x_k), slack recovery -----------------------------------
-  if constexpr (RB) {   // four right-hand sides per pass: a node's P row, dh / Fx blend and slack weights loaded once
-    constexpr int NB4 = 4;
+  if constexpr (RB) {   // BMPC_TS_POST_RB (4) right-hand sides per pass: a node's P row, dh / Fx blend and slack weights loaded once
+    constexpr int NB4 = BMPC_TS_POST_RB;
     struct VR { double v[NB4]; };
     for (int rb = 0; rb < nr; rb += NB4) {
       const int rn = nr - rb < NB4 ? nr - rb : NB4;
@@ -2440,12 +2449,6 @@ BMPC_HD auto coup_mem(const X& ex, gdouble* ws, CLayout& L, CPlan& P, int off) {
 template <class X>
 BMPC_HD auto coup_vec(const X& ex, int off) { return ex.lds + off; }
 
-// right-hand sides from which the coupling tree solve takes the post-pass that loads a node's
-// data once per four right-hand sides (tree_solve<..., RB=true>); a separate instantiation
-// with the same arithmetic per right-hand side (tests/test_kernel_host.py compares the two)
-#ifndef BMPC_TS_POST_RB_MIN
-#define BMPC_TS_POST_RB_MIN 8
-#endif
 
 // global variable index -> position in the primal vector
 BMPC_HD int gvar(CPlan& P, int i) { return i == P.ng - 1 ? P.oJ : P.oRho + i; }

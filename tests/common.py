@@ -42,13 +42,20 @@ from bmpc.scenarios import (LANES, highway_desc, highway_desc_from_golden, highw
 def unique_mask(T, NB, N, m, Nc=5, n=4, d=2):
     """Solution entries that are unique at the optimum: everything except the slacks of the
     leaf terminal nodes, which appear in no cost and no constraint but -S <= 0
-    (MPC_branch.py:1886-1892 only fills rows i < len(utraj); SURVEY quirk register)."""
+    (MPC_branch.py:1886-1892 only fills rows i < len(utraj); SURVEY quirk register), and, on
+    NB = 2 trees, the CVaR auxiliaries (rho, sigma, mu+, mu-; MPC_branch.py:1752-1804, 1940-1967):
+    there the interior point's choice moves along a flat direction of them at the rounding floor
+    (N=30 NB=2, step 1: the same 3e-4 relative difference on six mu entries of one branch point,
+    every other entry <= 1e-10)."""
     from oracle.tree import Topology
     t = Topology.build(N, NB, m)
     bd = t.bdim
-    oS = T * n + t.U * d + bd * (2 * m + 2)
+    oRho = T * n + t.U * d
+    oS = oRho + bd * (2 * m + 2)
     nv = oS + T * Nc + 1
     mask = np.ones(nv, bool)
+    if NB >= 2:
+        mask[oRho:oS] = False
     for b in range(t.nbranch):
         if t.is_leaf(b):
             k = t.ndx[b] + N

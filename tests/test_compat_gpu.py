@@ -3,8 +3,11 @@ main_branch.py builds it (Init_MPC + PredictiveModel + BranchMPC_CVaR + Highway_
 reproduce the closed loop the reference recorded (tests/golden/highway_n8_nb2.npz, made by
 the reference's own tree/assembly code with the oracle solver behind the ecos stub).
 
-Tolerance: uPred[0] to 1e-4 while the reference step exited 0 (ECOS 1e-8 optimum), 5e-3
-on exit-10 ("inaccurate") steps; the ego state after each step to 1e-3."""
+Tolerance (round 5): uPred[0] to 1e-6 while the reference step exited 0 (ECOS 1e-8 optimum;
+every step of the recording does since the equilibration), 5e-3 on exit-10 ("inaccurate")
+steps; the ego state after each step to 1e-6, over 20 steps (the host build of the same loop
+stays within 2.1e-7 in uPred[0] and 3.6e-8 in the state over all 40 recorded steps,
+tests/test_dropin_mains.py)."""
 import numpy as np
 import pytest
 
@@ -36,11 +39,11 @@ def test_main_branch_overtake_scene(gpu):
     mpcParam = Init_MPC.initBranchMPC(n, d, N, NB, xRef, am, rm, N_lane, cons.W)
     mpc = MPC_branch.BranchMPC_CVaR(mpcParam, model, ralpha=0.9)
     env = Highway_env_branch.Highway_env(NV=2, mpc=mpc, N_lane=N_lane)
-    steps = 12
+    steps = 20
     for t in range(steps):
-        np.testing.assert_allclose(env.veh_set[0].state, g["traj_x"][t], atol=1e-3, err_msg=f"ego state, step {t}")
+        np.testing.assert_allclose(env.veh_set[0].state, g["traj_x"][t], atol=1e-6, err_msg=f"ego state, step {t}")
         u_set, x_set, xx_set, xPred, zPred, branch_w = env.step(t)
-        tol = 1e-4 if int(g["traj_exit"][t]) == 0 else 5e-3
+        tol = 1e-6 if int(g["traj_exit"][t]) == 0 else 5e-3
         np.testing.assert_allclose(u_set[0], g["traj_u"][t], atol=tol, err_msg=f"uPred[0], step {t}")
         assert mpc.feasible == 1
         assert len(xPred) == len(branch_w) == 12 and xPred[0].shape == (N + 1, n)

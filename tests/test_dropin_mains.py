@@ -96,6 +96,13 @@ def test_reference_main_branch_runs_unchanged(host_device, monkeypatch):
     state_rec, input_rec = recs[0][0], recs[0][1]
     assert np.all(np.isfinite(state_rec))
     assert np.all(np.abs(input_rec[0][:, 1]) <= 0.3 + 1e-6)     # steering-rate bound rm
+    # the scene is the one tools/gen_golden.py recorded through the reference's own controller
+    # (highway_n8_nb2): every step exits 0 there, and the closed loop holds to 1e-6
+    from common import golden
+    g = golden("highway_n8_nb2")
+    assert np.all(g["traj_exit"][:10] == 0)
+    np.testing.assert_allclose(input_rec[0][:10], g["traj_u"][:10], atol=1e-6)
+    np.testing.assert_allclose(state_rec[0][:9], g["traj_x"][1:10], atol=1e-6)
 
 
 def test_bt_is_live_after_solve(host_device):

@@ -101,7 +101,10 @@ def test_device_closed_loop_follows_reference(solver_path):
     from conftest import assert_solver_path
     assert_solver_path(pl, solver_path)
     for t in range(T):
-        np.testing.assert_allclose(xs[t], np.repeat(np.asarray(g["traj_x"][t])[None], B, 0), rtol=0, atol=1e-4,
+        # (steps 2-3 of the recording exit 10, "inaccurate": their optimum is defined only to ECOS's
+        # reduced 5e-5 gap, and the host build's uPred[0] moves 5e-5 there; the state then differs
+        # by 5e-6 and decays to ~1e-6 -- every other step exits 0 on both sides)
+        np.testing.assert_allclose(xs[t], np.repeat(np.asarray(g["traj_x"][t])[None], B, 0), rtol=0, atol=2e-5,
                                    err_msg=f"closed-loop x at step {t}")
         np.testing.assert_allclose(zs[t], np.repeat(np.asarray(g["traj_z"][t])[None], B, 0), rtol=0, atol=1e-9,
                                    err_msg=f"closed-loop z at step {t}")

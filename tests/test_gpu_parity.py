@@ -111,14 +111,14 @@ def test_batch_matches_host_build(gpu):
     assert np.mean(agree) >= 0.9, agree
 
 
-def _check_sample_against_oracle(r, N, NB, x, z, xref, tgt, egos):
+def _check_sample_against_oracle(r, N, NB, x, z, xref, tgt, egos, workers=None):
     """Each sampled ego re-solved by the CPU oracle (the ECOS-algorithm restatement on the
     reference's assembly, tests/oracle_pool.py): J to 1e-6 relative; uPred[0] to 1e-6 where
     both exit 0 (certified to the 1e-8 tolerances), else 5e-3 (ECOS's reduced
     "inaccurate" tolerances); exit codes agree on >= 90% of the sample (0 vs 10 is decided at
     the rounding floor).  Returns the number of egos both sides solved to exit 0."""
     from oracle_pool import solve_many
-    res = solve_many([(N, NB, tgt[e], xref[e], x[e], z[e]) for e in egos])
+    res = solve_many([(N, NB, tgt[e], xref[e], x[e], z[e]) for e in egos], workers=workers)
     agree, tight = 0, 0
     for e, (st, J, u0) in zip(egos, res):
         assert abs(r["J"][e] - J) <= 1e-6 * max(1, abs(r["J"][e])), (e, r["J"][e], J)
@@ -148,15 +148,16 @@ def test_full_batch_certified(gpu):
     egos = np.unique(np.concatenate([[0, 1, 777, 4095], np.random.default_rng(11).choice(B, 28, replace=False)]))
     assert len(egos) >= 32
     tight = _check_sample_against_oracle(r, 20, 1, x, z, xref, tgt, egos)
-    assert tight >= 0.8 * len(egos)
+    # with ECOS's equilibration 4009 of the 4096 seeded egos exit 0 (3739 without it, round 4)
+    assert tight >= 0.9 * len(egos)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_config3_full_batch_lean(gpu):
     """BASELINE config 3 (N=30, NB=2: 9 leaves, 13 cones, a 50 x 50 coupling system) at 4096
     egos: the launch takes the lean k_ipm (coupling system in the slab, 16 egos per CU); every
-    ego returns a feasible ECOS-class status and a finite plan, and 8 sampled egos agree with
-    the CPU oracle."""
+    ego returns a feasible ECOS-class status and a finite plan, and 32 sampled egos agree with
+    the CPU oracle (~45 s of oracle per ego, 12 worker processes)."""
     from bmpc import abi
     B = 4096
     x, z, xref, tgt = seeded_batch(B, seed=3)
@@ -166,8 +167,9 @@ def test_config3_full_batch_lean(gpu):
     assert pl.last_kernel() == abi.KERNEL_IPM_LEAN
     assert np.all(r["status"] >= 0), np.unique(r["status"], return_counts=True)
     assert np.all(np.isfinite(r["J"])) and np.all(np.isfinite(r["upred"]))
-    egos = np.unique(np.concatenate([[0, 4095], np.random.default_rng(12).choice(B, 6, replace=False)]))
-    _check_sample_against_oracle(r, 30, 2, x, z, xref, tgt, egos)
+    egos = np.unique(np.concatenate([[0, 4095], np.random.default_rng(12).choice(B, 30, replace=False)]))
+    assert len(egos) >= 32
+    _check_sample_against_oracle(r, 30, 2, x, z, xref, tgt, egos, workers=12)
 
 
 def test_quadruped_prox_replay_gpu(gpu, qp_path):
