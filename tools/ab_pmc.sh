@@ -69,3 +69,4 @@ for v in vs:
     print(f"PMC {v}: FETCH {res['FETCH_SIZE']*1024/1e9:.1f} GB  WRITE {res['WRITE_SIZE']*1024/1e9:.1f} GB  2F+W {gb:.1f} GB per warm k_ipm launch")
 PY
 find $out -name "*.csv" -delete
+find $out -type f -size +2M -delete   # keep what comes back under the 64 MiB merge limit
