@@ -36,6 +36,12 @@
 #ifndef BMPC_PAIR_REFINE
 #define BMPC_PAIR_REFINE 1   // the pair's refinement rounds share their correction tree solves
 #endif
+#ifndef BMPC_REFINE_CALLS
+#define BMPC_REFINE_CALLS 1  // 1: kkt_refine_pair's correction back halves are calls of their own
+#endif
+#ifndef BMPC_FLAT_PAIR
+#define BMPC_FLAT_PAIR 1     // 1: the IPM loop calls the pair's coupling solve and refinement directly
+#endif
 #ifndef BMPC_PAIR_BACK
 #define BMPC_PAIR_BACK 1     // kkt_solve_pair's two back halves in one pass over the Woodbury data
 #endif
@@ -2843,6 +2849,35 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
 // residual met the tolerance stops as kkt_refine stops it.  Each direction's operations are
 // kkt_refine's, in the same order (its scratch: the second halves of k_e1 / k_e2 / k_cx /
 // k_cy / k_cz).
+#if BMPC_REFINE_CALLS
+// kkt_refine_pair's correction back halves as calls of their own (a smaller refinement frame on
+// the kernel's deepest call chain)
+template <class X, int NX, int NU>
+BMPC_FN void refine_back_pair(const X ex, const Ctx Cin) {
+  const Ctx C = Cin.uniform();
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, neq = P.neq, nr = P.nrows;
+  gdouble* cx = ws + L.k_cx;
+  gdouble* cy = ws + L.k_cy;
+  gdouble* cz = ws + L.k_cz;
+  kkt_back_pair<X, NX, NU, true>(ex, C, ws + L.k_e1, ws + L.k_e2, nullptr, cx, cy, cz, ws + L.k_e1 + nv,
+                                 ws + L.k_e2 + neq, nullptr, cx + nv, cy + neq, cz + nr, false);
+}
+template <class X, int NX, int NU>
+BMPC_FN void refine_solve_one(const X ex, const Ctx Cin, int j) {
+  const Ctx C = Cin.uniform();
+  j = ex.uniform(j != 0) ? 1 : 0;
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, neq = P.neq, nr = P.nrows;
+  kkt_solve_once<X, NX, NU, true>(ex, C, ws + L.k_e1 + j * nv, ws + L.k_e2 + j * neq, nullptr, ws + L.k_cx + j * nv,
+                                  ws + L.k_cy + j * neq, ws + L.k_cz + j * nr, false, false);
+}
+#endif
+
 template <class X, int NX, int NU>
 BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, const gdouble* r2a, const gdouble* r3ha,
                              gdouble* dxa, gdouble* dya, gdouble* dza, const gdouble* r1b, const gdouble* r2b,
@@ -2895,12 +2930,20 @@ BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, cons
     gdouble* cz = ws + L.k_cz;
     if (ex.uniform(on[0] && on[1])) {   // both corrections: one tree solve, one back half
       tree_solve<X, NX, NU>(ex, C, 2, ws + L.k_e1, nv, ws + L.k_e2, neq, cx, nv, cy, neq);
+#if BMPC_REFINE_CALLS
+      refine_back_pair<X, NX, NU>(ex, C);
+#else
       kkt_back_pair<X, NX, NU, true>(ex, C, ws + L.k_e1, ws + L.k_e2, nullptr, cx, cy, cz, ws + L.k_e1 + nv,
                                      ws + L.k_e2 + neq, nullptr, cx + nv, cy + neq, cz + nr, false);
+#endif
     } else {
       const int j = on[0] ? 0 : 1;
+#if BMPC_REFINE_CALLS
+      refine_solve_one<X, NX, NU>(ex, C, j);
+#else
       kkt_solve_once<X, NX, NU, true>(ex, C, ws + L.k_e1 + j * nv, ws + L.k_e2 + j * neq, nullptr, cx + j * nv,
                                       cy + j * neq, cz + j * nr, false, false);
+#endif
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -2970,6 +3013,46 @@ BMPC_FN bool kkt_solve_pair(const X ex, const Ctx Cin, const gdouble* r1c, const
 #endif
   return true;
 }
+
+#if BMPC_FLAT_PAIR
+// kkt_solve_pair split so that the IPM loop calls the coupling solve and the pair's refinement
+// itself (one call level less on the deepest call chain: the scratch stack is the sum of the
+// frames along it): kkt_pair_rhs forms both right-hand sides' W^-1 / G' parts, kkt_pair_back the
+// two back halves.  Same operations in the same order as kkt_solve_pair.
+template <class X, int NX, int NU>
+BMPC_FN void kkt_pair_rhs(const X ex, const Ctx Cin, const gdouble* r1c, const gdouble* r1a, const gdouble* r3a) {
+  const Ctx C = Cin.uniform();
+  r1c = uniform_ptr(r1c), r1a = uniform_ptr(r1a), r3a = uniform_ptr(r3a);
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_KKT);
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, nc = P.ncones;
+  gdouble* tzc = ws + L.gk + nc * nv;
+  gdouble* tza = tzc + nv;
+  gdouble* tr = ws + L.k_r0;
+  apply_Winv2(ex, C, ws + L.hvec, ws + L.k_t3, tr);
+  apply_GT<X, NX, NU>(ex, C, tr, tzc, r1c);
+  apply_Winv2(ex, C, r3a, ws + L.k_t3b, tr);
+  apply_GT<X, NX, NU>(ex, C, tr, tza, r1a);
+  BMPC_COUNT(ws, L, PROF_NSOLVE);
+  BMPC_COUNT(ws, L, PROF_NSOLVE);
+}
+template <class X, int NX, int NU>
+BMPC_FN void kkt_pair_back(const X ex, const Ctx Cin, bool fin) {
+  const Ctx C = Cin.uniform();
+  fin = ex.uniform(fin);
+  CPlan& P = *C.P;
+  CLayout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_KKT);
+  gdouble* ws = C.ws;
+  const size_t nv = P.nv, nc = P.ncones;
+  const gdouble* tzc = ws + L.gk + nc * nv;
+  const gdouble* tza = tzc + nv;
+  kkt_back_pair<X, NX, NU>(ex, C, tzc, ws + L.bvec, ws + L.k_t3, ws + L.x1, ws + L.y1, ws + L.z1, tza, ws + L.ry,
+                           ws + L.k_t3b, ws + L.x2, ws + L.y2, ws + L.z2, fin);
+}
+#endif
 
 // ECOS bring2cone: s = r + (1 + alpha) e
 template <class X>
@@ -3456,7 +3539,17 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return i == P.oJ ? -1.0 : 0.0; }, [&](int i, double v) { tA[i] = v; });
       lane_batch<16>(ex, 0, nv, [&](int i) { return -rx[i]; }, [&](int i, double v) { tA2[i] = v; });
       apply_W(ex, C, 0, lam, rb, 1.0, rz, 1.0);
+#if BMPC_FLAT_PAIR
+      kkt_pair_rhs<X, NX, NU>(ex, C, tA, tA2, rb);
+      ok = ex.uniform(kkt_coupling<X, NX, NU>(ex, C, 2));
+      if (ok) {
+        kkt_pair_back<X, NX, NU>(ex, C, nref == 0);
+        if (nref > 0)
+          kkt_refine_pair<X, NX, NU>(ex, C, tA, bv, ws + L.k_t3, x1, y1, z1, tA2, ry, ws + L.k_t3b, x2, y2, z2, nref);
+      }
+#else
       ok = ex.uniform(kkt_solve_pair<X, NX, NU>(ex, C, tA, tA2, rb, nref));
+#endif
     }
     if (ok) {
       const double den = kap / tau - (x1[P.oJ] + dot2(ex, bv, y1, neq, hv, z1, nr));
