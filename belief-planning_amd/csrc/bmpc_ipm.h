@@ -3049,8 +3049,13 @@ BMPC_FN void kkt_pair_back(const X ex, const Ctx Cin, bool fin) {
   const size_t nv = P.nv, nc = P.ncones;
   const gdouble* tzc = ws + L.gk + nc * nv;
   const gdouble* tza = tzc + nv;
+#if BMPC_PAIR_BACK
   kkt_back_pair<X, NX, NU>(ex, C, tzc, ws + L.bvec, ws + L.k_t3, ws + L.x1, ws + L.y1, ws + L.z1, tza, ws + L.ry,
                            ws + L.k_t3b, ws + L.x2, ws + L.y2, ws + L.z2, fin);
+#else
+  kkt_back<X, NX, NU, false>(ex, C, tzc, ws + L.bvec, ws + L.k_t3, ws + L.x1, ws + L.y1, ws + L.z1, fin);
+  kkt_back<X, NX, NU, false>(ex, C, tza, ws + L.ry, ws + L.k_t3b, ws + L.x2, ws + L.y2, ws + L.z2, fin);
+#endif
 }
 #endif
 
@@ -3544,8 +3549,14 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       ok = ex.uniform(kkt_coupling<X, NX, NU>(ex, C, 2));
       if (ok) {
         kkt_pair_back<X, NX, NU>(ex, C, nref == 0);
-        if (nref > 0)
+        if (nref > 0) {
+#if BMPC_PAIR_REFINE
           kkt_refine_pair<X, NX, NU>(ex, C, tA, bv, ws + L.k_t3, x1, y1, z1, tA2, ry, ws + L.k_t3b, x2, y2, z2, nref);
+#else
+          kkt_refine<X, NX, NU>(ex, C, tA, bv, ws + L.k_t3, x1, y1, z1, nref);
+          kkt_refine<X, NX, NU>(ex, C, tA2, ry, ws + L.k_t3b, x2, y2, z2, nref);
+#endif
+        }
       }
 #else
       ok = ex.uniform(kkt_solve_pair<X, NX, NU>(ex, C, tA, tA2, rb, nref));

@@ -165,6 +165,18 @@ def test_paired_solves_are_bit_identical():
             assert np.array_equal(a[k], b[k]), (N, NB, k)
 
 
+def test_flat_call_chain_is_bit_identical():
+    """The IPM loop calls the pair's coupling solve and refinement itself (BMPC_FLAT_PAIR) and
+    the refinement's correction back halves are calls of their own (BMPC_REFINE_CALLS): only
+    the call structure differs from the nested kkt_solve_pair build, so the bits are the same."""
+    import numpy as np
+    for B, N, NB, steps in ((24, 20, 1, 2), (4, 30, 2, 1)):
+        a = _seeded_closed_loop("", B, N, NB, steps)
+        b = _seeded_closed_loop("-DBMPC_FLAT_PAIR=0 -DBMPC_REFINE_CALLS=0", B, N, NB, steps)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (N, NB, k)
+
+
 def test_batched_post_pass_is_bit_identical():
     """The coupling tree solve of NB = 2 plans (15 right-hand sides) takes the post-pass that
     loads a node's data once per four right-hand sides (tree_solve<..., RB=true>, from
