@@ -36,8 +36,9 @@ def sources():
     """Translation units of libbmpc.so: the C ABI + small kernels, one unit per predictive model's
     solver kernels (compiled in parallel), the host-side plan builders."""
     srcs = [os.path.join(CSRC, f) for f in ("bmpc_hip.hip", "bmpc_k_highway.hip", "bmpc_k_highway_t.hip",
-                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_plan.cpp",
-                                            "bmpc_qpplan.cpp")]
+                                            "bmpc_k_merge.hip", "bmpc_k_quadruped.hip", "bmpc_kb_highway.hip",
+                                            "bmpc_kb_highway_t.hip", "bmpc_kb_merge.hip", "bmpc_kb_quadruped.hip",
+                                            "bmpc_plan.cpp", "bmpc_qpplan.cpp")]
     if _phased():
         srcs += [os.path.join(EXPERIMENTAL, f) for f in ("bmpc_kp_highway.hip", "bmpc_kp_highway_t.hip",
                                                          "bmpc_kp_merge.hip")]

@@ -41,8 +41,15 @@ namespace bmpc {
 // through the scalar cache), the per-wave scratch is LDS (ldouble).  On the host build the
 // qualifiers vanish.
 // ------------------------------------------------------------------------------------
+// The small-batch kernel's translation units (bmpc_kb_*.hip) define BMPC_FLAT_SLAB: their slab
+// pointers are generic (flat loads and stores), so that a per-ego layout can place the IPM's
+// most-visited arrays in the workgroup's LDS (bmpc_dev.h, k_solve_blk).
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(BMPC_FLAT_SLAB)
+#define BMPC_AS_GLOBAL
+#else
 #define BMPC_AS_GLOBAL __attribute__((address_space(1)))
+#endif
 #define BMPC_AS_LDS __attribute__((address_space(3)))
 #define BMPC_AS_CONST __attribute__((address_space(4)))
 #else

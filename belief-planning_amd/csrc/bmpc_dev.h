@@ -257,21 +257,56 @@ __device__ __forceinline__ DevBlockExecT<TR, true, NW> solver_exec_blk(const Pla
 
 // One ego per workgroup of NW waves (small batches: every wave of the chip on few egos);
 // QP: the OSQP-class controllers' k_qp path, else the CVaR IPM.
+//
+// LDS-resident arrays (lay != NULL; translation units with BMPC_FLAT_SLAB only): lay[e] is ego e's
+// copy of the layout in which spans of the IPM's own arrays (written before they are read within a
+// solve: the NT scaling, the node factors and tree-solve vectors, z / s / lambda) are offset from
+// the ego's slab to this workgroup's LDS at hot_off doubles (flat addresses: LDS aperture + offset,
+// bmpc_hip.hip blk_layouts); the tree's linearisation (A, B and dh, written by k_tree) is copied
+// in when its span is relocated.  A layout that does not land in this workgroup's LDS fails the
+// solve with EXIT_GUARD.
 template <class M, bool QP, int NW>
 __global__ __launch_bounds__(64 * NW) void k_solve_blk(const Bundle* __restrict__ B, double* __restrict__ ws,
                                                       const bmpc_policy* __restrict__ pol, double* upred,
                                                       double* xpred, double* bw, double* J, int32_t* status,
-                                                      int32_t* iters, int batch) {
+                                                      int32_t* iters, int batch, const Layout* __restrict__ lay,
+                                                      size_t hot_off) {
   const int e = blockIdx.x;
   if (e >= batch) return;
   const Plan& P = B->P;
-  const Layout& L = B->L;
+  const Layout& L0 = B->L;
+  const Layout& L = lay ? lay[e] : L0;
   constexpr bool TR = QP ? false : M::kTransform;
   extern __shared__ double lds_dyn[];
   const auto ex = solver_exec_blk<TR, NW>(P, lds_dyn);
   using X = DevBlockExecT<TR, true, NW>;
-  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+#if defined(BMPC_FLAT_SLAB)
+  // the slab pointer through readfirstlane: the compiler cannot infer from the kernel argument
+  // that the arrays behind it are global memory, so every slab access is a flat access (LDS or
+  // global by address)
+  EgoView E{uniform_ptr(ws + L0.stride * (size_t)e), pol + (size_t)e * P.m};
+#else
+  EgoView E{ws + L0.stride * (size_t)e, pol + (size_t)e * P.m};
+#endif
   IpmResult r;
+#if defined(BMPC_FLAT_SLAB)
+  if (lay) {
+    const int t = threadIdx.x, nt = 64 * NW;
+    double* w = E.ws;
+    if ((uintptr_t)(w + L.dl) != (uintptr_t)(lds_dyn + hot_off)) {   // the first relocated span
+      if (t == 0) {
+        if (status) status[e] = EXIT_GUARD;
+        if (iters) iters[e] = 0;
+      }
+      return;
+    }
+    if (L.Ad != L0.Ad)
+      for (size_t i = t; i < L0.Cd - L0.Ad; i += nt) w[L.Ad + i] = w[L0.Ad + i];
+    if (L.dh != L0.dh)
+      for (size_t i = t; i < L0.h0 - L0.dh; i += nt) w[L.dh + i] = w[L0.dh + i];
+    __syncthreads();
+  }
+#endif
   if constexpr (QP) r = solve_ego_qp<X, M>(ex, P, L, E);
   else r = solve_ego_ipm<X, M>(ex, P, L, E);
   const double* w = E.ws;
@@ -374,6 +409,8 @@ struct SolveLaunch {
   bool qp;            // OSQP-class controller (k_qp) instead of the CVaR IPM (k_ipm)
   hipStream_t stream;
   int nw = 4;        // small-batch launch: waves per ego (4 or 8)
+  const Layout* blk_lay = nullptr;   // ... per-ego layouts with LDS-resident spans (or NULL)
+  size_t blk_hot_off = 0;            // ... their LDS offset (doubles)
 #if defined(BMPC_WITH_PHASED)
   // phase-per-kernel IPM (experimental/bmpc_dev_ph.h, tools-only builds): per-iteration "egos
   // going on" counters, their pinned read-back slot, the iteration limit, the sub-batch streams
@@ -424,7 +461,7 @@ hipError_t launch_blk_kernel(const SolveLaunch& a) {
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL((k_solve_blk<M, QP, NW>), dim3(a.batch), dim3(64 * NW), a.lds_bytes, a.stream, a.bundle, a.ws,
-                     a.pol, a.upred, a.xpred, a.bw, a.J, a.status, a.iters, a.batch);
+                     a.pol, a.upred, a.xpred, a.bw, a.J, a.status, a.iters, a.batch, a.blk_lay, a.blk_hot_off);
   return hipGetLastError();
 }
 // (the OSQP-class controllers never take this path: bmpc_hip.hip chooses it for the CVaR IPM only)

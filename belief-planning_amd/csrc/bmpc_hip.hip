@@ -221,6 +221,8 @@ struct bmpc_ctx {
   int device;
   int cus;             // compute units (hipDeviceProp_t::multiProcessorCount)
   size_t lds_per_cu;   // LDS bytes per CU (maxSharedMemoryPerMultiProcessor)
+  size_t lds_per_block = 0;      // LDS bytes one workgroup may opt in to (sharedMemPerBlockOptin)
+  unsigned long long lds_flat0 = 0;   // flat address of LDS offset 0 (k_lds_aperture), 0 = not probed
   // bmpc_qp_solve: its own stream (synchronised alone, never the device), the analysis cache
   // and grow-only buffers reused across calls
   hipStream_t qstream = nullptr;
@@ -265,6 +267,10 @@ struct bmpc_plan {
   bool pol_on_device = false;   // bmpc_env_step re-targeted d_pol: h_pol is stale
   int last_kernel = BMPC_KERNEL_NONE;   // solver kernel of the last launch (BMPC_INFO_SOLVER)
   double* d_lref = nullptr;   // lane reference of the *_PSIREF policies (grid | values)
+  // small-batch kernel: per-ego layouts with LDS-resident spans (blk_layouts), built on the first
+  // small-batch solve for this plan's LDS base
+  Layout* d_blk_lay = nullptr;
+  size_t blk_lay_base = 0, blk_hot_off = 0, blk_hot_bytes = 0;
   bool psiref = false;        // some policy in force tracks the lane reference
 #if defined(BMPC_WITH_PHASED)
   int32_t* d_count = nullptr;   // phase-per-kernel IPM: egos going on per iteration [kMaxSub][maxit + 1]
@@ -306,6 +312,7 @@ int bmpc_open(int hip_device, bmpc_ctx** out) {
   c->device = hip_device;
   c->cus = cus;
   c->lds_per_cu = lds;
+  c->lds_per_block = prop.sharedMemPerBlockOptin > 0 ? std::min(prop.sharedMemPerBlockOptin, lds) : lds;
   *out = c;
   return 0;
 }
@@ -381,6 +388,7 @@ int bmpc_plan_destroy(bmpc_plan* pl) {
   hipFree(pl->d_iout);
   hipFree(pl->d_scratch);
   hipFree(pl->d_lref);
+  hipFree(pl->d_blk_lay);
   for (auto& e : pl->ev)
     if (e) hipEventDestroy(e);
 #if defined(BMPC_WITH_PHASED)
@@ -504,6 +512,82 @@ static int use_phased() {
 }
 #endif
 
+// the flat (generic) address of LDS offset 0: the LDS aperture base every workgroup's LDS is
+// addressed through (the same for every kernel of the process)
+__global__ void k_lds_aperture(unsigned long long* out) {
+  __shared__ double s[2];
+  s[threadIdx.x & 1] = 0.0;
+  if (threadIdx.x == 0) out[0] = (unsigned long long)(uintptr_t)(double*)s;
+}
+
+// LDS-resident spans of the small-batch kernel (bmpc_dev.h, k_solve_blk): ego e's layout with
+// spans of the IPM's own arrays offset from the ego's slab (d_ws + e * stride) to the workgroup's
+// LDS after the launch's own lds_base bytes.  Spans in priority order, each kept whole (code
+// addresses several fields of a span from one base) and skipped when it does not fit: the NT
+// scaling (dl .. vnt), the node factors (hx .. kff), the tree solve's l and x right-hand sides
+// (lvec, qx0), z / s / lambda, the tree's A / B and dh (copied in by the kernel).  Every span
+// holds arrays a solve writes before it reads them (or that the kernel copies in); the scaling's
+// span must fit (the kernel's guard checks it).  Returns the extra LDS bytes (0: no layouts).
+static int blk_layouts(bmpc_plan* pl, size_t lds_base) {
+  bmpc_ctx* c = pl->ctx;
+  if (pl->d_blk_lay && pl->blk_lay_base == lds_base) return 0;
+  if (!c->lds_flat0) {
+    unsigned long long* d = nullptr;
+    HIPCHECK(hipMalloc(&d, sizeof(unsigned long long)));
+    hipLaunchKernelGGL(k_lds_aperture, dim3(1), dim3(64), 0, pl->stream, d);
+    unsigned long long h = 0;
+    hipError_t e = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, pl->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(pl->stream);
+    hipFree(d);
+    HIPCHECK(e);
+    if (!h) return fail(-5, "LDS aperture probe returned 0");
+    c->lds_flat0 = h;
+  }
+  const Layout& L = pl->hp.lay;
+  const size_t off0 = ((lds_base + 63) & ~(size_t)63) / sizeof(double);
+  const size_t cap = c->lds_per_block / sizeof(double);
+  struct Span { size_t Layout::*a; size_t Layout::*b; };
+  const Span spans[] = {{&Layout::dl, &Layout::hx},   {&Layout::hx, &Layout::lvec}, {&Layout::lvec, &Layout::qx0},
+                        {&Layout::qx0, &Layout::gk},  {&Layout::z, &Layout::z1},    {&Layout::Ad, &Layout::Cd},
+                        {&Layout::dh, &Layout::h0}};
+  const int nsp = sizeof(spans) / sizeof(spans[0]);
+  size_t at[nsp];   // LDS offset (doubles) of each relocated span, 0 = stays in the slab
+  size_t cur = off0;
+  for (int k = 0; k < nsp; ++k) {
+    const size_t a = L.*spans[k].a, b = L.*spans[k].b;
+    at[k] = 0;
+    if (b <= a) continue;
+    const size_t len = (b - a + 7) & ~(size_t)7;
+    if (cur + len <= cap) {
+      at[k] = cur;
+      cur += len;
+    }
+  }
+  if (!at[0]) return 0;   // not even the scaling fits: the plain layout
+  const int B = pl->batch;
+  std::vector<Layout> lays(B, L);
+  const size_t nf = offsetof(Layout, stride) / sizeof(size_t);
+  for (int e = 0; e < B; ++e) {
+    const int64_t ws_e = (int64_t)(uintptr_t)(pl->d_ws + (size_t)e * L.stride);
+    size_t* f = reinterpret_cast<size_t*>(&lays[e]);
+    const size_t* f0 = reinterpret_cast<const size_t*>(&L);
+    for (int k = 0; k < nsp; ++k) {
+      if (!at[k]) continue;
+      const size_t a = L.*spans[k].a, b = L.*spans[k].b;
+      // ws_e + 8 (off + delta) = LDS(at[k] + off - a) for every field offset off in [a, b)
+      const int64_t delta = ((int64_t)c->lds_flat0 + 8 * (int64_t)at[k] - ws_e) / 8 - (int64_t)a;
+      for (size_t i = 0; i < nf; ++i)
+        if (f0[i] >= a && f0[i] < b) f[i] = (size_t)((int64_t)f0[i] + delta);
+    }
+  }
+  if (!pl->d_blk_lay) HIPCHECK(hipMalloc(&pl->d_blk_lay, sizeof(Layout) * (size_t)B));
+  HIPCHECK(hipMemcpy(pl->d_blk_lay, lays.data(), sizeof(Layout) * (size_t)B, hipMemcpyHostToDevice));
+  pl->blk_lay_base = lds_base;
+  pl->blk_hot_off = at[0];
+  pl->blk_hot_bytes = (cur - off0) * sizeof(double);
+  return 0;
+}
+
 static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, const double* d_xref,
                         double* d_upred, double* d_xpred, double* d_bw, double* d_J,
                         int32_t* d_status, int32_t* d_iters, hipStream_t s) {
@@ -547,6 +631,16 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
     if (const char* e = getenv("BMPC_BLOCK_WAVES")) a.nw = atoi(e) == 8 ? 8 : 4;
     a.lds_bytes = solver_lds_bytes_blk(P, xform, a.nw);
     a.rich = true;
+    // BMPC_BLK_LDS=0: the small-batch kernel keeps every array in the slab
+    const char* el = getenv("BMPC_BLK_LDS");
+    if (!(el && atoi(el) == 0)) {
+      if (const int rc = blk_layouts(pl, a.lds_bytes)) return rc;
+      if (pl->d_blk_lay) {
+        a.blk_lay = pl->d_blk_lay;
+        a.blk_hot_off = pl->blk_hot_off;
+        a.lds_bytes = pl->blk_hot_off * sizeof(double) + pl->blk_hot_bytes;
+      }
+    }
     kernel = a.nw == 8 ? BMPC_KERNEL_IPM_BLK8 : BMPC_KERNEL_IPM_BLK4;
     if (hwt) solver = launch_solver_blk_highway_t;
     else if (P.desc.model == BMPC_MODEL_HIGHWAY) solver = launch_solver_blk_highway;

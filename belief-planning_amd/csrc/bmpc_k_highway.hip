@@ -7,7 +7,5 @@ namespace dev {
 hipError_t launch_tree_highway(const SolveLaunch& a) { return launch_tree<Highway>(a); }
 hipError_t launch_solver_highway(const SolveLaunch& a) { return launch_solver<Highway, true>(a); }
 
-hipError_t launch_solver_blk_highway(const SolveLaunch& a) { return launch_solver_blk<Highway, true>(a); }
-
 }  // namespace dev
 }  // namespace bmpc

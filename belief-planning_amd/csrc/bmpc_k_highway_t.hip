@@ -7,7 +7,5 @@ namespace dev {
 hipError_t launch_tree_highway_t(const SolveLaunch& a) { return launch_tree<HighwayT>(a); }
 hipError_t launch_solver_highway_t(const SolveLaunch& a) { return launch_solver<HighwayT, false>(a); }
 
-hipError_t launch_solver_blk_highway_t(const SolveLaunch& a) { return launch_solver_blk<HighwayT, false>(a); }
-
 }  // namespace dev
 }  // namespace bmpc

@@ -7,7 +7,5 @@ namespace dev {
 hipError_t launch_tree_merge(const SolveLaunch& a) { return launch_tree<HighwayMerge>(a); }
 hipError_t launch_solver_merge(const SolveLaunch& a) { return launch_solver<HighwayMerge, false>(a); }
 
-hipError_t launch_solver_blk_merge(const SolveLaunch& a) { return launch_solver_blk<HighwayMerge, false>(a); }
-
 }  // namespace dev
 }  // namespace bmpc

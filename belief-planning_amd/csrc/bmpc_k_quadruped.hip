@@ -7,7 +7,5 @@ namespace dev {
 hipError_t launch_tree_quadruped(const SolveLaunch& a) { return launch_tree<Quadruped>(a); }
 hipError_t launch_solver_quadruped(const SolveLaunch& a) { return launch_solver<Quadruped, true>(a); }
 
-hipError_t launch_solver_blk_quadruped(const SolveLaunch& a) { return launch_solver_blk<Quadruped, true>(a); }
-
 }  // namespace dev
 }  // namespace bmpc
