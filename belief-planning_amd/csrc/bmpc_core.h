@@ -301,9 +301,38 @@ BMPC_HD void strided_batch(int first, int stride, int hi, Ld ld, St st) {
   }
 }
 
+// Executors that spread one ego over several waves (the small-batch kernel's DevBlockExecT:
+// kBatchDiv = its waves) give each lane that many times fewer elements of a pass: their batches
+// shrink by the same factor, so a pass issues its loads for the elements a lane has instead of
+// UN clamped slots (per lane the stores still come in index order: the same values, the same
+// order of any accumulation in st).
+template <class X, class = void>
+struct BatchDiv {
+  static constexpr int v = 1;
+};
+template <class X>
+struct BatchDiv<X, decltype((void)X::kBatchDiv)> {
+  static constexpr int v = X::kBatchDiv;
+};
+
+template <int UN, class X>
+struct Narrow {
+  static constexpr int v = UN / BatchDiv<X>::v > 0 ? UN / BatchDiv<X>::v : 1;
+};
+// the batch width of a cone group's strided loops (4; the small-batch kernel's executor may
+// set kConeBatch for its wider cone groups)
+template <class X, class = void>
+struct ConeBatch {
+  static constexpr int v = 4;
+};
+template <class X>
+struct ConeBatch<X, decltype((void)X::kConeBatch)> {
+  static constexpr int v = X::kConeBatch;
+};
+
 template <int UN = 8, class X, class Ld, class St>
 BMPC_HD void lane_batch(const X& ex, int lo, int hi, Ld ld, St st) {
-  strided_batch<UN>(lo + ex.lane, ex.nlanes, hi, ld, st);
+  strided_batch<Narrow<UN, X>::v>(lo + ex.lane, ex.nlanes, hi, ld, st);
 }
 
 // per-lane partial reduction of f(i) over first, first+stride, ... < hi with UN
@@ -337,13 +366,19 @@ BMPC_HD double strided_partial(int first, int stride, int hi, F f) {
 
 template <int UN = 8, class X, class F>
 BMPC_HD double lane_partial(const X& ex, int lo, int hi, F f) {
-  return strided_partial<UN, 0>(lo + ex.lane, ex.nlanes, hi, f);
+  return strided_partial<Narrow<UN, X>::v, 0>(lo + ex.lane, ex.nlanes, hi, f);
+}
+
+// this lane's max (OP 1) / min (OP 2) of f(i) over its indices of [lo, hi)
+template <int UN, int OP, class X, class F>
+BMPC_HD double lane_extreme(const X& ex, int lo, int hi, F f) {
+  return strided_partial<Narrow<UN, X>::v, OP>(lo + ex.lane, ex.nlanes, hi, f);
 }
 
 // sum over the lanes of f(i), i in [lo, hi)
 template <int UN = 8, class X, class F>
 BMPC_HD double lane_sum(const X& ex, int lo, int hi, F f) {
-  return ex.sum(strided_partial<UN, 0>(lo + ex.lane, ex.nlanes, hi, f));
+  return ex.sum(strided_partial<Narrow<UN, X>::v, 0>(lo + ex.lane, ex.nlanes, hi, f));
 }
 
 // Cone groups: the lanes split into groups of cg lanes (a power of two); group g handles

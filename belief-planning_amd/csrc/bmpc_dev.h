@@ -130,9 +130,13 @@ struct DevBlockExecT {
   ldouble* eco;
   ldouble* red;   // reduction scratch: kRedMax * NW doubles
   static constexpr int nlanes = 64 * NW;
+  static constexpr int kBatchDiv = NW;   // lane batches NW times narrower (bmpc_core.h, lane_batch)
   static constexpr bool kRowLanes = true;
   static constexpr int kTaskLanes = 4;
-  static constexpr int kConeRegRows = 8;
+  // wider cone groups than one wave's (exec_cgrp): fewer rows per lane in the fused cone passes
+  // and the cone groups' strided loops (4 waves: a 122-row cone on 64 lanes holds 2 rows a lane)
+  static constexpr int kConeRegRows = NW == 4 ? 4 : 8;
+  static constexpr int kConeBatch = NW == 4 ? 2 : 4;
   static constexpr int kRedMax = 16;
   __device__ double tsum(double v) const {
     v += dpp_d<0xB1>(v);

@@ -291,7 +291,7 @@ BMPC_HD void cone_supp_gdx2(const X& ex, CPlan& P, const T& t, const gdouble* g0
 // ------------------------------------------------------------------------------------
 template <class X>
 BMPC_HD double cone_dot(const X ex, const ConeGroups& G, const gdouble* a, const gdouble* b, int off, int q) {
-  return ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) { return a[off + i] * b[off + i]; }), G.cg);
+  return ex.gsum(strided_partial<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) { return a[off + i] * b[off + i]; }), G.cg);
 }
 
 // v0^2 - ||v1||^2 without squaring the dominant entry (see oracle.ecos_ipm.cone_res)
@@ -318,7 +318,7 @@ BMPC_HD double cone_res(const X ex, const ConeGroups& G, const gdouble* v, int o
   const double gm = ex.gmax(amax, G.cg);
   const double kd = ex.gmin(amax == gm && aidx < 1e300 ? aidx : 1e300, G.cg);
   const int kidx = kd < 1e300 ? (int)kd : -1;
-  const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
+  const double ss = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) {
     const double t = v[off + i];
     return (i == kidx ? 0.0 : 1.0) * (t * t);
   }), G.cg);
@@ -556,7 +556,7 @@ BMPC_HD void apply_G_body(const X ex, const Ctx Cin, const gdouble* zv, gdouble*
         out[off] = f;
         out[off + q - 1] = -f;
       }
-      strided_batch<4>(G.gl, G.cg, nmid, mid, [&](int it, double v) { out[off + 1 + it] = v; });
+      strided_batch<ConeBatch<X>::v>(G.gl, G.cg, nmid, mid, [&](int it, double v) { out[off + 1 + it] = v; });
     } else {
       // the cone's rows of G zv in registers (q = nmid + 2), then W^-1 (and again for WM = 2)
       const double f0 = ex.gsum(G.gl == 0 ? f : 0.0, G.cg);
@@ -879,7 +879,7 @@ BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s
   gdouble* wb = C.at(C.L->wbar);
   gdouble* vn = C.at(C.L->vnt);
   struct DL { double d, l; };
-  double bad = strided_partial<8, 1>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
+  double bad = lane_extreme<8, 1>(ex, 0, P.nlp, [&](int i) {
     const double si = s[i], zi = z[i];   // both loaded: no short-circuit branch around z's load
     return ((si > 0.0) & (zi > 0.0)) ? 0.0 : 1.0;
   });
@@ -902,14 +902,14 @@ BMPC_FN_SCALING bool compute_scaling(const X ex, const Ctx Cin, const gdouble* s
     const double nrm = sqrt(2.0 * (w0 + 1.0));
     const double e = sqrt(sn / zn);
     // v'z without storing v first: v_i = (wbar_i + [i==0]) / nrm
-    const double vz = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
+    const double vz = ex.gsum(strided_partial<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
       const double zi = z[off + i];
       const double jz = i == 0 ? zi : -zi;
       const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
       return (w + (i == 0 ? 1.0 : 0.0)) / nrm * z[off + i];
     }), G.cg);
     struct WV { double w, v, l; };
-    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+    strided_batch<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
       const double zi = z[off + i];
       const double jz = i == 0 ? zi : -zi;
       const double w = (s[off + i] / sn + jz / zn) / (2.0 * gam);
@@ -1001,11 +1001,11 @@ BMPC_HD void apply_W(const X ex, const Ctx& C, int mode, const gdouble* in, gdou
         if (i < q) out[off + i] = sc * (2.0 * av[uu] * dot - (i == 0 ? in0 : -iv[uu])) + sa * adv[uu];
       }
     } else {                // long cones: dot pass, then write pass
-      const double dot = ex.gsum(strided_partial<4>(G.gl, G.cg, q, [&](int i) {
+      const double dot = ex.gsum(strided_partial<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
         const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
         return ai * in[off + i];
       }), G.cg);
-      strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+      strided_batch<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
         const double ai = (jconj && i > 0) ? -a[off + i] : a[off + i];
         const double jv = i == 0 ? in0 : -in[off + i];
         return sc * (2.0 * ai * dot - jv) + sa * ad[off + i];
@@ -1024,7 +1024,7 @@ BMPC_HD void jprod(const X ex, const Ctx& C, const gdouble* u, const gdouble* v,
     BMPC_CONE_K(P, G, k, off, q);
     const double dot = cone_dot(ex, G, u, v, off, q);
     const double u0 = q > 0 ? u[off] : 0.0, v0 = q > 0 ? v[off] : 0.0;
-    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+    strided_batch<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
       const double m0 = i == 0 ? 1.0 : 0.0;   // blend, not a select around the loads
       return m0 * dot + (1.0 - m0) * (u0 * v[off + i] + v0 * u[off + i]);
     }, [&](int i, double r) { out[off + i] = r; });
@@ -1040,11 +1040,11 @@ BMPC_HD void jdiv(const X ex, const Ctx& C, const gdouble* lam, const gdouble* v
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double rho = cone_res(ex, G, lam, off, q);
-    const double lv = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * v[off + i]; }),
+    const double lv = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * v[off + i]; }),
                               G.cg);
     const double l0 = q > 0 ? lam[off] : 1.0;
     const double x0 = q > 0 ? (l0 * v[off] - lv) / rho : 0.0;
-    strided_batch<4>(G.gl, G.cg, q, [&](int i) {
+    strided_batch<ConeBatch<X>::v>(G.gl, G.cg, q, [&](int i) {
       const double m0 = i == 0 ? 1.0 : 0.0;
       return m0 * x0 + (1.0 - m0) * ((v[off + i] - x0 * lam[off + i]) / l0);
     }, [&](int i, double r) { out[off + i] = r; });
@@ -1058,19 +1058,19 @@ BMPC_FN_MAX_STEP double max_step(const X ex, const Ctx Cin, const gdouble* lam, 
   const Ctx C = Cin.uniform();
   CPlan& P = *C.P;
   // -lam / min(d, -0): the ratio where d < 0, +inf elsewhere (no branch around the division)
-  double a = strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) { return -lam[i] / fmin(d[i], -0.0); });
+  double a = lane_extreme<8, 2>(ex, 0, P.nlp, [&](int i) { return -lam[i] / fmin(d[i], -0.0); });
   double bad = 0.0;
   BMPC_CONE_ROUNDS(ex, P, G) {
     BMPC_CONE_K(P, G, k, off, q);
     const double ln2 = cone_res(ex, G, lam, off, q);
     if (!(ln2 > 0.0)) bad = 1.0;
     const double ln = sqrt(ln2);
-    const double ld = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
+    const double ld = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
                               G.cg);
     const double lb0 = q > 0 ? lam[off] / ln : 0.0;
     const double rho0 = q > 0 ? (lam[off] * d[off] - ld) / ln : 0.0;
     const double fac = q > 0 ? (rho0 + d[off]) / (lb0 + 1.0) : 0.0;
-    const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
+    const double ss = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) {
       const double r1 = d[off + i] - fac * lam[off + i] / ln;
       return r1 * r1;
     }), G.cg);
@@ -1088,7 +1088,7 @@ BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam,
   CPlan& P = *C.P;
   struct A2 { double a, b; };
   double a1 = 1e300, a2 = 1e300;
-  strided_batch<8>(ex.lane, ex.nlanes, P.nlp, [&](int i) {
+  lane_batch<8>(ex, 0, P.nlp, [&](int i) {
     const double l = lam[i], u = d1[i], v = d2[i];
     return A2{-l / fmin(u, -0.0), -l / fmin(v, -0.0)};   // +inf where the direction is >= 0
   }, [&](int, A2 r) { a1 = fmin(a1, r.a); a2 = fmin(a2, r.b); });
@@ -1100,11 +1100,11 @@ BMPC_FN_MAX_STEP double max_step2(const X ex, const Ctx Cin, const gdouble* lam,
     const double ln = sqrt(ln2);
     const double lb0 = q > 0 ? lam[off] / ln : 0.0;
     auto one = [&](const gdouble* d, double& a) {
-      const double ld = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
+      const double ld = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) { return lam[off + i] * d[off + i]; }),
                                 G.cg);
       const double rho0 = q > 0 ? (lam[off] * d[off] - ld) / ln : 0.0;
       const double fac = q > 0 ? (rho0 + d[off]) / (lb0 + 1.0) : 0.0;
-      const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) {
+      const double ss = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) {
         const double r1 = d[off + i] - fac * lam[off + i] / ln;
         return r1 * r1;
       }), G.cg);
@@ -2356,7 +2356,7 @@ BMPC_FN bool small_lu(const X ex, PM* M, PP* piv, int n) {
     // read-modify-writes, a memory round trip each when the system lives in the slab); each
     // entry gets the same single update M_ij - l_i M_kj as before
     const int m = n - k - 1;
-    strided_batch<8>(ex.lane, ex.nlanes, m * m, [&](int t) {
+    lane_batch<8>(ex, 0, m * m, [&](int t) {
       const int i = k + 1 + t / m, j = k + 1 + t % m;
       return M[i * n + j] - M[i * n + k] * M[k * n + j];
     }, [&](int t, double v) { M[(k + 1 + t / m) * n + k + 1 + t % m] = v; });
@@ -2807,7 +2807,7 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
   // the scale max(|r1|, |r2|, |r3h|) and the residual's max norm are taken in the passes that
   // read r1 / r2 and write e1 / e2 (max is exact: the same values as separate passes); the |r3h|
   // part before the first round
-  double msc = nitref == 0 ? 0.0 : strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[i]); });
+  double msc = nitref == 0 ? 0.0 : lane_extreme<8, 1>(ex, 0, P.nrows, [&](int i) { return fabs(r3h[i]); });
   double sc = 0.0;
   for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
@@ -2899,7 +2899,7 @@ BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, cons
   double msc[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)   // kkt_refine's scale and residual norms, per direction
-    msc[j] = nitref == 0 ? 0.0 : strided_partial<8, 1>(ex.lane, ex.nlanes, P.nrows, [&](int i) { return fabs(r3h[j][i]); });
+    msc[j] = nitref == 0 ? 0.0 : lane_extreme<8, 1>(ex, 0, P.nrows, [&](int i) { return fabs(r3h[j][i]); });
   bool on[2] = {true, true};
   for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
@@ -3064,13 +3064,13 @@ template <class X>
 BMPC_HD void bring2cone(const X ex, const Ctx& C, const gdouble* r, gdouble* s) {
   CPlan& P = *C.P;
   double alpha = -0.99;
-  const double mn = -ex.min(strided_partial<8, 2>(ex.lane, ex.nlanes, P.nlp, [&](int i) { return r[i]; }));
+  const double mn = -ex.min(lane_extreme<8, 2>(ex, 0, P.nlp, [&](int i) { return r[i]; }));
   if (P.nlp > 0 && mn >= 0.0 && mn > alpha) alpha = mn;
   {
     double worst = -1e300;   // max over cones of -(r0 - ||r1||) where r0 - ||r1|| <= 0
     BMPC_CONE_ROUNDS(ex, P, G) {
       BMPC_CONE_K(P, G, k, off, q);
-      const double ss = ex.gsum(strided_partial<4>(1 + G.gl, G.cg, q, [&](int i) { return r[off + i] * r[off + i]; }),
+      const double ss = ex.gsum(strided_partial<ConeBatch<X>::v>(1 + G.gl, G.cg, q, [&](int i) { return r[off + i] * r[off + i]; }),
                                 G.cg);
       const double cres = q > 0 ? r[off] - sqrt(ss) : 1.0;
       if (cres <= 0.0) worst = fmax(worst, -cres);
