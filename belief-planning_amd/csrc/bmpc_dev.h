@@ -459,10 +459,15 @@ hipError_t launch_solver(const SolveLaunch& a) {
 // the small-batch launch: one ego per NW-wave workgroup (solver_lds_bytes_blk of LDS)
 template <class M, bool QP, int NW>
 hipError_t launch_blk_kernel(const SolveLaunch& a) {
-  if (a.lds_bytes > 64 * 1024) {
+  // the opt-in is a driver call of its own (~1.5 ms per one-ego solve when made on every launch):
+  // made once per device and size
+  static size_t opted[16] = {};
+  int dev = 0;
+  if (a.lds_bytes > 64 * 1024 && hipGetDevice(&dev) == hipSuccess && a.lds_bytes > opted[dev & 15]) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_solve_blk<M, QP, NW>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds_bytes);
     if (e != hipSuccess) return e;
+    opted[dev & 15] = a.lds_bytes;
   }
   hipLaunchKernelGGL((k_solve_blk<M, QP, NW>), dim3(a.batch), dim3(64 * NW), a.lds_bytes, a.stream, a.bundle, a.ws,
                      a.pol, a.upred, a.xpred, a.bw, a.J, a.status, a.iters, a.batch, a.blk_lay, a.blk_hot_off);
