@@ -114,11 +114,14 @@ struct DevExecT {
 
 using DevExec = DevExecT<false>;
 
+#ifndef BMPC_BLK_RED2
+#define BMPC_BLK_RED2 1   // whole-executor reductions with one barrier (two buffers in turn)
+#endif
 // Multi-wave executor: one ego on NW waves of one workgroup (batch-1 / small-batch callers --
 // main_branch's one solve per step): the same phase templates with 64*NW lanes, so the tree
 // solve's tasks, the cone groups and every lane loop spread over NW waves.  Wave-level
 // operations (DPP quads, cone-group shuffles) are unchanged; whole-executor reductions go
-// through LDS (`red`, K*NW doubles) between two barriers.
+// through LDS (`red`: K*NW doubles of one of two buffers) and one barrier.
 template <bool TR, bool TL, int NW>
 struct DevBlockExecT {
   static constexpr bool kTransform = TR;
@@ -128,7 +131,7 @@ struct DevBlockExecT {
   ldouble* lds;
   tab_ptr tab;
   ldouble* eco;
-  ldouble* red;   // reduction scratch: kRedMax * NW doubles
+  ldouble* red;   // reduction scratch: 2 * kRedMax * NW doubles, then NW turn slots
   static constexpr int nlanes = 64 * NW;
   static constexpr int kBatchDiv = NW;   // lane batches NW times narrower (bmpc_core.h, lane_batch)
   static constexpr bool kRowLanes = true;
@@ -171,17 +174,32 @@ struct DevBlockExecT {
         v[k] = OP == 0 ? v[k] + w : OP == 1 ? fmax(v[k], w) : fmin(v[k], w);
       }
     const int wv = lane >> 6;
+#if BMPC_BLK_RED2
+    // two buffers used in turn (each wave's turn kept in its LDS slot: every wave runs the same
+    // reductions in the same order): a wave writing reduction r + 2 into the buffer of r has
+    // passed r + 1's barrier, which every wave reaches only after reading r -- one barrier each
+    ldouble* turn = red + 2 * kRedMax * NW + wv;
+    const int odd = __builtin_amdgcn_readfirstlane((int)*turn);
+    ldouble* buf = red + (odd ? kRedMax * NW : 0);
+    if ((lane & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) buf[k * NW + wv] = v[k];
+      *turn = odd ? 0.0 : 1.0;
+    }
+#else
+    ldouble* buf = red;
     __syncthreads();   // the previous reduction's readers are done with red
     if ((lane & 63) == 0)
 #pragma unroll
       for (int k = 0; k < K; ++k) red[k * NW + wv] = v[k];
+#endif
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      double a = red[k * NW];
+      double a = buf[k * NW];
 #pragma unroll
       for (int w = 1; w < NW; ++w) {
-        const double b = red[k * NW + w];
+        const double b = buf[k * NW + w];
         a = OP == 0 ? a + b : OP == 1 ? fmax(a, b) : fmin(a, b);
       }
       v[k] = a;
@@ -244,7 +262,7 @@ __device__ __forceinline__ DevExecT<TR, TL> solver_exec(const Plan& P, double* l
 
 // LDS of a multi-wave solver launch: the wave launch's, then the reduction scratch
 __host__ __device__ inline size_t solver_lds_bytes_blk(const Plan& P, bool transform, int nw) {
-  return ((solver_lds_bytes(P, transform, true) + 7) & ~(size_t)7) + sizeof(double) * 16 * (size_t)nw;
+  return ((solver_lds_bytes(P, transform, true) + 7) & ~(size_t)7) + sizeof(double) * (2 * 16 + 1) * (size_t)nw;
 }
 template <bool TR, int NW>
 __device__ __forceinline__ DevBlockExecT<TR, true, NW> solver_exec_blk(const Plan& P, double* lds_dyn) {
@@ -255,6 +273,7 @@ __device__ __forceinline__ DevBlockExecT<TR, true, NW> solver_exec_blk(const Pla
   for (int i = t; i < P.ntab; i += nt) tabl[i] = gtab[i];
   double* eco = lds_dyn + (solver_lds_bytes(P, false, true) / sizeof(double));
   double* red = lds_dyn + ((solver_lds_bytes(P, TR, true) + 7) & ~(size_t)7) / sizeof(double);
+  if (t < NW) red[2 * 16 * NW + t] = 0.0;   // each wave's reduction turn (BMPC_BLK_RED2)
   __syncthreads();
   return DevBlockExecT<TR, true, NW>{t, (ldouble*)lds_dyn, (lint*)tabl, (ldouble*)eco, (ldouble*)red};
 }
