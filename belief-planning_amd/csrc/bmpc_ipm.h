@@ -36,6 +36,9 @@
 #ifndef BMPC_PAIR_REFINE
 #define BMPC_PAIR_REFINE 1   // the pair's refinement rounds share their correction tree solves
 #endif
+#ifndef BMPC_BLK_WAVE_SUBST
+#define BMPC_BLK_WAVE_SUBST 1   // multi-wave executors: the coupling substitutions on one wave
+#endif
 #ifndef BMPC_REFINE_CALLS
 #define BMPC_REFINE_CALLS 1  // 1: kkt_refine_pair's correction back halves are calls of their own
 #endif
@@ -2411,6 +2414,51 @@ BMPC_HD void small_lu_solve_rows(const X ex, const PM* M, PB* b, int n) {
   }
 }
 
+// small_lu_solve_rows on the first wave of a multi-wave executor alone: its rows' steps ordered
+// by wave-scope fences instead of one workgroup barrier each (3n barriers per solve; the other
+// waves wait at the caller's one barrier).  Same operations in the same order.
+BMPC_HD inline void wave_sync() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+template <class PM, class PB>
+BMPC_HD void small_lu_solve_rows_wave(int j, const PM* M, PB* b, int n) {
+  const bool row = j < n;
+  const size_t rj = (size_t)(row ? j : 0) * n;
+  for (int i0 = 0; i0 < n; i0 += 8) {   // L (unit diagonal)
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i0 + u < n ? i0 + u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < n) {
+        const double bi = b[i];
+        if (row && j > i) b[j] -= mc[u] * bi;
+        wave_sync();
+      }
+    }
+  }
+  for (int i1 = n - 1; i1 >= 0; i1 -= 8) {   // U
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i1 - u >= 0 ? i1 - u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i1 - u;
+      if (i >= 0) {
+        if (j == i) b[i] = b[i] / mc[u];
+        wave_sync();
+        const double bi = b[i];
+        if (row && j < i) b[j] -= mc[u] * bi;
+        wave_sync();
+      }
+    }
+  }
+}
+
 // solve with the LU above; b in LDS, column-oriented substitution (one step per row)
 template <class X, class PM, class PP, class PB>
 BMPC_HD void small_lu_solve(const X ex, const PM* M, const PP* piv, PB* b, int n) {
@@ -2425,6 +2473,15 @@ BMPC_HD void small_lu_solve(const X ex, const PM* M, const PP* piv, PB* b, int n
     }
   ex.sync();
   if constexpr (RowLanes<X>::value) {
+#if BMPC_BLK_WAVE_SUBST
+    if constexpr (X::nlanes > 64) {
+      if (n <= 64) {
+        if (ex.lane < 64) small_lu_solve_rows_wave(ex.lane, M, b, n);
+        ex.sync();
+        return;
+      }
+    }
+#endif
     if (n <= X::nlanes) {
       small_lu_solve_rows(ex, M, b, n);
       return;
