@@ -2417,7 +2417,7 @@ BMPC_HD void small_lu_solve_rows(const X ex, const PM* M, PB* b, int n) {
 // small_lu_solve_rows on the first wave of a multi-wave executor alone: its rows' steps ordered
 // by wave-scope fences instead of one workgroup barrier each (3n barriers per solve; the other
 // waves wait at the caller's one barrier).  Same operations in the same order.
-BMPC_HD inline void wave_sync() {
+BMPC_HD void wave_sync() {
 #if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
