@@ -284,8 +284,27 @@ struct ProfScope {
 // The loads are unconditional (an index past hi is clamped to b, which is valid): a load
 // under a per-lane guard would sit in its own exec-masked block with its own wait, i.e. one
 // memory round trip per element instead of one per batch.
+#ifndef BMPC_TAIL_BATCH
+#define BMPC_TAIL_BATCH 1   // lane batches: full batches, then halving ones (no clamped duplicate loads)
+#endif
 template <int UN = 8, class Ld, class St>
 BMPC_HD void strided_batch(int first, int stride, int hi, Ld ld, St st) {
+#if BMPC_TAIL_BATCH
+  // full batches of UN while all of a lane's UN slots are in range, the rest in halving
+  // batches (16 + 4 slots for 20 elements instead of 32): no clamped duplicate loads; a lane
+  // still visits its indices in increasing order
+  int b = first;
+  for (; b + (UN - 1) * stride < hi; b += UN * stride) {
+    decltype(ld(b)) v[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) v[u] = ld(b + u * stride);
+#pragma unroll
+    for (int u = 0; u < UN; ++u) st(b + u * stride, v[u]);
+  }
+  if constexpr (UN > 1) strided_batch<UN / 2>(b, stride, hi, ld, st);
+  else if (b < hi) st(b, ld(b));
+  return;
+#endif
   for (int b = first; b < hi; b += UN * stride) {
     decltype(ld(b)) v[UN];
 #pragma unroll
