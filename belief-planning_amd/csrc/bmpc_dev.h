@@ -347,8 +347,16 @@ __global__ __launch_bounds__(64 * NW) void k_solve_blk(const Bundle* __restrict_
   }
 }
 
+#ifndef BMPC_TREE_WPE
+#define BMPC_TREE_WPE 4   // k_tree's register budget: 4 waves per SIMD (k_tree 1.23 -> 0.99 ms at 4,096 egos, r05ad; 3: 1.30)
+#endif
+#if BMPC_TREE_WPE > 0
+#define BMPC_TREE_ATTR __attribute__((amdgpu_waves_per_eu(BMPC_TREE_WPE)))
+#else
+#define BMPC_TREE_ATTR
+#endif
 template <class M>
-__global__ __launch_bounds__(64) void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
+__global__ __launch_bounds__(64) BMPC_TREE_ATTR void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
                                              const bmpc_policy* __restrict__ pol,
                                              const double* __restrict__ x, const double* __restrict__ z,
                                              const double* __restrict__ xref, int batch) {
