@@ -348,15 +348,13 @@ __global__ __launch_bounds__(64 * NW) void k_solve_blk(const Bundle* __restrict_
 }
 
 #ifndef BMPC_TREE_WPE
-#define BMPC_TREE_WPE 4   // k_tree's register budget: 4 waves per SIMD (k_tree 1.23 -> 0.99 ms at 4,096 egos, r05ad; 3: 1.30)
+#define BMPC_TREE_WPE 4   // k_tree's register budget in batches beyond 2 waves per SIMD (r05ad: 1.23 -> 0.99 ms at 4,096 egos; 3: 1.30)
 #endif
-#if BMPC_TREE_WPE > 0
-#define BMPC_TREE_ATTR __attribute__((amdgpu_waves_per_eu(BMPC_TREE_WPE)))
-#else
-#define BMPC_TREE_ATTR
-#endif
-template <class M>
-__global__ __launch_bounds__(64) BMPC_TREE_ATTR void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
+// WPE: waves per SIMD the register budget allows (1: 2 waves, the compiler's own choice of 220 VGPRs).  The
+// budget pays where the batch has more egos than 2 waves per SIMD hold (launch_tree); a one-ego
+// launch is faster without its spills.
+template <class M, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE > 1 ? WPE : 2))) void k_tree(const Bundle* __restrict__ B, double* __restrict__ ws,
                                              const bmpc_policy* __restrict__ pol,
                                              const double* __restrict__ x, const double* __restrict__ z,
                                              const double* __restrict__ xref, int batch) {
@@ -441,6 +439,7 @@ struct SolveLaunch {
   hipStream_t stream;
   int nw = 4;        // small-batch launch: waves per ego (4 or 8)
   const Layout* blk_lay = nullptr;   // ... per-ego layouts with LDS-resident spans (or NULL)
+  int cus = 256;                     // compute units of the device (k_tree's register budget)
   size_t blk_hot_off = 0;            // ... their LDS offset (doubles)
 #if defined(BMPC_WITH_PHASED)
   // phase-per-kernel IPM (experimental/bmpc_dev_ph.h, tools-only builds): per-iteration "egos
@@ -457,7 +456,11 @@ struct SolveLaunch {
 
 template <class M>
 hipError_t launch_tree(const SolveLaunch& a) {
-  hipLaunchKernelGGL(k_tree<M>, dim3(a.batch), dim3(64), 0, a.stream, a.bundle, a.ws, a.pol, a.x, a.z, a.xref,
+  if (BMPC_TREE_WPE > 1 && a.batch > 2 * 4 * a.cus)
+    hipLaunchKernelGGL((k_tree<M, (BMPC_TREE_WPE > 1 ? BMPC_TREE_WPE : 1)>), dim3(a.batch), dim3(64), 0, a.stream,
+                       a.bundle, a.ws, a.pol, a.x, a.z, a.xref, a.batch);
+  else
+    hipLaunchKernelGGL((k_tree<M, 1>), dim3(a.batch), dim3(64), 0, a.stream, a.bundle, a.ws, a.pol, a.x, a.z, a.xref,
                      a.batch);
   return hipGetLastError();
 }
