@@ -148,13 +148,38 @@ def load(path: str = SO_PATH, strict: bool = True):
     return lib
 
 
+def stamp(path: str = SO_PATH):
+    """The source hash a library was compiled from (its ``<so>.srchash`` sidecar), or None."""
+    try:
+        with open(path + ".srchash") as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
+def check_stamp(path: str = SO_PATH) -> str:
+    """Refuse a product library that was not compiled from the sources in this tree: its stamp
+    must equal source_hash().  Returns the stamp."""
+    have, want = stamp(path), source_hash()
+    if have != want:
+        raise BmpcUnavailable(f"{path} is stale: built from sources {have or '<no stamp>'}, the tree's sources "
+                              f"hash to {want}; rebuild with __graft_entry__.build()")
+    return have
+
+
+LOADED_STAMP = None     # stamp of the library lib() loaded (bench.py reports it)
+
+
 def lib():
-    """The product library; BMPC_LIBRARY may name another in-tree build of the same
-    sources (e.g. libbmpc_prof.so for phase counters)."""
-    global _LIB
+    """The product library, refused when its stamp does not match the tree's sources;
+    BMPC_LIBRARY may name another in-tree build (e.g. libbmpc_prof.so for phase counters,
+    an older source for an A/B), which is loaded without the check."""
+    global _LIB, LOADED_STAMP
     if _LIB is None:
         path = os.environ.get("BMPC_LIBRARY", SO_PATH)
-        _LIB = load(path, strict=os.path.abspath(path) == os.path.abspath(SO_PATH))
+        product = os.path.abspath(path) == os.path.abspath(SO_PATH)
+        LOADED_STAMP = check_stamp(path) if product else stamp(path)
+        _LIB = load(path, strict=product)
     return _LIB
 
 

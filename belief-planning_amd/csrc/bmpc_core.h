@@ -277,6 +277,23 @@ struct ProfScope {
 #endif
 
 // ------------------------------------------------------------------------------------
+// iteration trace of the IPMs (diagnostics builds only): -DBMPC_HOST_DEBUG on the host build,
+// -DBMPC_DEV_DEBUG on the device (lane 0 of workgroup 0 -- trace a one-ego batch), the same
+// format on both so tools/trace_diff.py can line them up
+// ------------------------------------------------------------------------------------
+#if defined(BMPC_HOST_DEBUG) && !defined(__HIP_DEVICE_COMPILE__)
+#define BMPC_TRACING 1
+#define BMPC_TRACE(...) printf(__VA_ARGS__)
+#elif defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__)
+#define BMPC_TRACING 1
+#define BMPC_TRACE(...) \
+  do { if (blockIdx.x == 0 && threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define BMPC_TRACING 0
+#define BMPC_TRACE(...) ((void)0)
+#endif
+
+// ------------------------------------------------------------------------------------
 // batched lane loops: every lane first evaluates ld(i) for up to UN of its indices -- all
 // loads of the batch are in flight together instead of one memory round trip per element
 // -- then commits them with st(i, v).  ld must not read what st of the same batch writes.

@@ -2887,9 +2887,7 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
     if (itr == 0) sc = ex.max(msc);
     const double err = ex.max(merr);
     ex.sync();
-#ifdef BMPC_HOST_DEBUG
-    printf("   refine %d err %.3e sc %.3e\n", itr, err, sc);
-#endif
+    BMPC_TRACE("   refine %d err %.3e sc %.3e\n", itr, err, sc);
     if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
     kkt_solve_once<X, NX, NU, true>(ex, C, e1, e2, nullptr, cx, cy, cz, false, false);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
@@ -2980,6 +2978,7 @@ BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, cons
       const double err = ex.max(merr);
       ex.sync();
       on[j] = ex.uniform(err > BMPC_REFTOL * fmax(sc[j], 1.0));
+      BMPC_TRACE("   refine[%d] %d err %.3e sc %.3e\n", j, itr, err, sc[j]);
     }
     if (!ex.uniform(on[0] || on[1])) break;
     gdouble* cx = ws + L.k_cx;
@@ -3561,22 +3560,15 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i]; }, [&](int i, double v) { ws[L.bestx + i] = v; });
       ex.sync();
     }
-#if defined(BMPC_HOST_DEBUG) || (defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__))
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (blockIdx.x == 0 && ex.lane == 0)
-#endif
-    printf("it %3d pcost %+.9e dcost %+.9e gap %.2e pres %.2e dres %.2e k/t %.2e tau %.2e nx %.2e ny %.2e nz %.2e ns %.2e"
-           " best %.3e maxit %d\n",
-           it, pcost, dcost, gap, pres, dres, kap / tau, tau, nx, ny, nz, ns, best_score, P.desc.maxit);
-#endif
+    BMPC_TRACE("it %3d pcost %+.16e dcost %+.16e gap %.16e pres %.16e dres %.16e kap %.16e tau %.16e"
+               " nx %.16e ny %.16e nz %.16e ns %.16e best %.3e\n",
+               it, pcost, dcost, gap, pres, dres, kap, tau, nx, ny, nz, ns, best_score);
     int code = check(feastol, abstol, reltol);
     if (code == 99 && it == P.desc.maxit) {
       const int c2 = check(1e-4, 5e-5, 5e-5);
       code = c2 == 99 ? EXIT_MAXIT : c2 + EXIT_INACC;
     }
-#if defined(BMPC_DEV_DEBUG) && defined(__HIP_DEVICE_COMPILE__)
-    if (blockIdx.x == 0 && ex.lane == 0) printf("   code %d (it %d)\n", code, it);
-#endif
+    if (code != 99) BMPC_TRACE("   code %d (it %d)\n", code, it);
     if (code != 99) {
       lane_batch<16>(ex, 0, nv, [&](int i) { return x[i] / tau; }, [&](int i, double v) { ws[L.sol + i] = v; });
       ex.sync();
@@ -3659,6 +3651,8 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       alpha = a * 0.99;           // never step onto or past the cone / tau / kappa boundary
       const double fin = ex.max(nonfinite);
       ok = ex.uniform(fin == 0.0 && isfinite(dtau) && alpha > 1e-10);
+      BMPC_TRACE("   step den %.16e dtau_a %.16e a_aff %.16e sigma %.16e dtau %.16e alpha %.16e nref %d ok %d\n",
+                 den, dtau_a, a_aff, sigma, dtau, alpha, nref, (int)ok);
       if (ok) {
         lane_batch<8>(ex, 0, nv, [&](int i) { return x[i] + (alpha * x2[i]); }, [&](int i, double v) { x[i] = v; });
         lane_batch(ex, 0, neq, [&](int i) { return y[i] + (alpha * y2[i]); }, [&](int i, double v) { y[i] = v; });
@@ -3671,6 +3665,7 @@ BMPC_HD IpmResult ipm_solve(const X ex, const Ctx& C) {
       }
     }
     if (!ok) {   // numerical failure: ECOS backtracks to the best iterate
+      BMPC_TRACE("   backtrack (it %d) to the best iterate (it %d, score %.3e)\n", it, best_it, best_score);
       // guard: the best iterate's score and tau are held in registers across every phase call
       // of the loop; a build whose register allocation lost them is reported
       // as EXIT_GUARD instead of returning a wrong point

@@ -11,6 +11,10 @@
 
 #include "bmpc_model.h"
 
+#ifndef BMPC_CONE_BOOST
+#define BMPC_CONE_BOOST 1   // 0: boost 0 on every cone (A/B of the rotated-cone row boost)
+#endif
+
 namespace bmpc {
 
 struct EgoView {
@@ -158,7 +162,7 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
         est += uv[r] * q;
       }
     }
-    boost[k] = 0.5 * log(est > 1.0 ? est : 1.0);
+    boost[k] = BMPC_CONE_BOOST ? 0.5 * log(est > 1.0 ? est : 1.0) : 0.0;
   }
   ex.sync();
 }

@@ -402,14 +402,18 @@ def main():
         hbm_alg = B * abytes / kern_s / 1e9 if kern_s > 0 else 0.0
         key = f"{a.workload}:N{a.N}:NB{a.NB}:B{B}"
         src = _lib.source_hash()
+        lib_stamp = None if host else _lib.LOADED_STAMP   # lib() refused the product .so unless == src
         traffic, tsrc = load_traffic(a.traffic, key, src)
         kname = "k_qp (structured Mehrotra QP IPM)" if (quad or robust) else "k_ipm (structured HSDE IPM)"
+        headline = not (quad or robust) and (a.N, a.NB, B) == (20, 1, 4096)
         out = {
-            "metric": (METRIC if not (quad or robust) else
-                       "branch-MPC solves/sec (whole node), quadruped BranchMPCProx N=25 NB=2 m=2 (4 leaves), "
-                       "batch 1024 egos" if quad else
+            "metric": (METRIC if headline else
+                       f"branch-MPC solves/sec (whole node), quadruped BranchMPCProx N={a.N} NB={a.NB} m=2 "
+                       f"({2 ** a.NB} leaves), batch {B} egos" if quad else
                        f"robustMPC solves/sec (whole node), highway N={a.N} NB={a.NB}, {3 ** a.NB} obstacle "
-                       f"predictions per slot, batch {B} egos"),
+                       f"predictions per slot, batch {B} egos" if robust else
+                       f"branch-MPC solves/sec (whole node), highway N={a.N} NB={a.NB} ({3 ** a.NB} leaves), "
+                       f"batch {B} egos"),
             "value": round(value, 2), "unit": "solves/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 4),
             "higher_is_better": True, "scaling": "weak" if not a.global_batch else "strong",
@@ -425,6 +429,7 @@ def main():
             "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),
                          "traffic": traffic, "traffic_source": tsrc, "traffic_key": key, "source_hash": src,
+                         "library_stamp": lib_stamp,
                          "hbm_alg_GBps": round(hbm_alg, 4), "hbm_frac": round(hbm_alg / (HBM_PEAK_TBPS * 1e3), 9),
                          "alg_bytes_per_solve": abytes,
                          "hbm_traffic_frac": (round(traffic / kern_s / (HBM_PEAK_TBPS * 1e12), 4)

@@ -18,11 +18,27 @@ algorithm (Domahidi, Chu, Boyd, "ECOS: An SOCP solver for embedded systems", ECC
   numerically (ECOS backtracks to its best iterate), inaccurate if the best iterate meets
   the reduced tolerances, else -1 / -2.  No other early exit.
 
+* ECOS's Ruiz equilibration of [A; G] (``ECOS_setup``, ECOS 2.0.x ``equil.c``; :func:`equilibration`).
+
 Linear algebra is a sparse LU of the full KKT matrix
 ``[[0, A', G'], [A, 0, 0], [G, 0, -W'W]]`` (ECOS uses a sparse LDL' with static
 regularisation; the solution of the KKT system is the same) with iterative refinement.
 Parity of the *iterates* against ECOS is unpinned (no recorded ECOS output exists);
 the returned point is certified by its own KKT residuals.
+
+**Declared non-ECOS ingredient: the rotated-cone row boost** (:func:`boost_rows`, applied after
+the equilibration).  The CVaR cones' first and last rows are (1 - a, ..., 1 + a) with |a| up to
+~1e3 (``MPC_branch.py:1948-1964``); the oracle and the kernel (``k_tree`` writes the per-cone
+beta = 1/2 log(max(1, sum xbar'Q xbar + ubar'R ubar)), ``oracle.tree.CVaRController.cone_boost``)
+pre-multiply those two rows by the Lorentz boost T_beta, a cone automorphism: the feasible set,
+the optimum and the returned (unboosted) x, y, z, s are unchanged, but the NT scaling, the initial
+point and the exit tests' residual norms are formed in the boosted coordinates.  ECOS has no such
+step.  Kept after the round-6 A/B (``tools/boost_experiment.py``, ``profiles/r06/boost_ab.log``):
+with equilibration on and beta = 0 this restatement reaches ECOS's full tolerances on 1 of the 26
+solver problems the six CVaR recordings hold (25 with the boost) at 46.7 iterations on average
+(29.9): the boost is what makes this restatement's (and the kernel's) unscaled cone arithmetic
+reach 1e-8 on these rows.  The recordings' exit codes are therefore those of ECOS's algorithm
+plus this boost.
 """
 from __future__ import annotations
 

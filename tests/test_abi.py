@@ -76,3 +76,35 @@ def test_alternate_builds_load_non_strictly(tmp_path):
     assert lib.bmpc_abi_version() == 2
     with pytest.raises(_lib.BmpcUnavailable):
         lib.bmpc_set_lane_ref(None, 0, None, None)
+
+
+def test_lib_refuses_a_stale_product_library(tmp_path, monkeypatch):
+    """lib() loads the product libbmpc.so only when its <so>.srchash stamp equals the hash of the
+    sources in the tree (a stale prebuilt binary would otherwise be measured and reported under
+    the current source's hash); another build named by BMPC_LIBRARY is exempt."""
+    import shutil
+    import pytest
+    from bmpc import _lib
+    _lib.build()
+    so = tmp_path / "libbmpc.so"
+    shutil.copy(_lib.SO_PATH, so)
+    (tmp_path / "libbmpc.so.srchash").write_text("0123456789abcdef\n")
+    monkeypatch.setattr(_lib, "SO_PATH", str(so))
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.delenv("BMPC_LIBRARY", raising=False)
+    with pytest.raises(_lib.BmpcUnavailable, match="stale"):
+        _lib.lib()
+    (tmp_path / "libbmpc.so.srchash").unlink()
+    with pytest.raises(_lib.BmpcUnavailable, match="no stamp"):
+        _lib.lib()
+    (tmp_path / "libbmpc.so.srchash").write_text(_lib.source_hash() + "\n")
+    assert _lib.lib() is not None and _lib.LOADED_STAMP == _lib.source_hash()
+    # an A/B build named by BMPC_LIBRARY loads whatever its stamp says
+    monkeypatch.setattr(_lib, "_LIB", None)
+    other = tmp_path / "libother.so"
+    shutil.copy(_lib.SO_PATH, other)
+    (tmp_path / "libother.so.srchash").write_text("feedfeedfeedfeed\n")
+    monkeypatch.setenv("BMPC_LIBRARY", str(other))
+    _lib.lib()
+    assert _lib.LOADED_STAMP == "feedfeedfeedfeed"
+    monkeypatch.setattr(_lib, "_LIB", None)

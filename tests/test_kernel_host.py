@@ -27,6 +27,12 @@ def check_replay(r, g, T, tree=None, min_agree=0.9):
     J = np.asarray(g["traj_J"][:T])
     u = np.asarray(g["traj_u"][:T])
     assert np.all(r["status"] >= 0), r["status"]
+    both0 = (exits == 0) & (r["status"] == 0)
+    relJ = np.abs(r["J"] - J) / np.maximum(1.0, np.abs(J))
+    du0 = np.max(np.abs(r["upred"][:, 0] - u), axis=1)
+    print(f"replay {g['N']}/{g['NB']}: exit codes agree on {int(np.sum(r['status'] == exits))} of {T} steps "
+          f"(exit 10 recorded {int(np.sum(exits == 10))}, got {int(np.sum(r['status'] == 10))}); both exit 0: "
+          f"max rel |dJ| {relJ[both0].max() if both0.any() else 0:.1e}, max |du0| {du0[both0].max() if both0.any() else 0:.1e}")
     # ECOS exit 0 vs 10 is decided at the 1e-8 rounding floor; most steps must agree exactly (the
     # host build >= 95%; the GPU's summation orders flip 2 of the 20 N=10 steps on the one-wave
     # kernels, round 5)

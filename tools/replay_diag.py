@@ -23,5 +23,7 @@ for name in ("highway_n20_nb1", "highway_n8_nb2", "highway_n10_nb1", "highway_n3
     rel = np.abs(r["J"] - J) / np.maximum(1, np.abs(J))
     print(f"{name}: T={T} exit agree {np.mean(r['status'] == ex):.3f}  ref10 {int((ex == 10).sum())} "
           f"got10 {int((r['status'] == 10).sum())}  max relJ {rel.max():.2e}  iters {r['iters'][:6]}")
+    bad = np.nonzero(r["status"] != ex)[0]
+    print(f"   kernel {pl.last_kernel()}  steps whose exit differs: {bad.tolist()} (got {r['status'][bad].tolist()})")
     if T <= 5:
         print("   status", r["status"], "ref", ex, "J", r["J"], "refJ", J)
