@@ -36,8 +36,10 @@ point and the exit tests' residual norms are formed in the boosted coordinates. 
 step.  Kept after the round-6 A/B (``tools/boost_experiment.py``, ``profiles/r06/boost_ab.log``):
 with equilibration on and beta = 0 this restatement reaches ECOS's full tolerances on 1 of the 26
 solver problems the six CVaR recordings hold (25 with the boost) at 46.7 iterations on average
-(29.9): the boost is what makes this restatement's (and the kernel's) unscaled cone arithmetic
-reach 1e-8 on these rows.  The recordings' exit codes are therefore those of ECOS's algorithm
+(29.9), on none of 288 seeded closed-loop solves (223 with it; 43.0 vs 27.0 iterations), and the
+kernel algorithm (host build, -DBMPC_CONE_BOOST=0) on 9 of the 184 recorded highway steps (181 with
+it): the boost is what makes this restatement's (and the kernel's) cone arithmetic reach 1e-8 on
+these rows.  The recordings' exit codes are therefore those of ECOS's algorithm
 plus this boost.
 """
 from __future__ import annotations
