@@ -347,6 +347,38 @@ __global__ __launch_bounds__(64 * NW) void k_solve_blk(const Bundle* __restrict_
   }
 }
 
+#if defined(BMPC_BLK2)
+// Tools-only A/B (-DBMPC_BLK2, BMPC_IPM_W2=1): the large-batch CVaR IPM with one ego on TWO waves
+// (the small-batch kernel's executor at 128 lanes, slab arrays in global memory, the register
+// budget of k_ipm) -- 8 egos per CU instead of 16, each on twice the lanes.
+template <class M>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_ipm_w2(
+    const Bundle* __restrict__ B, double* __restrict__ ws, const bmpc_policy* __restrict__ pol, double* upred,
+    double* xpred, double* bw, double* J, int32_t* status, int32_t* iters, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  extern __shared__ double lds_dyn[];
+  const auto ex = solver_exec_blk<M::kTransform, 2>(P, lds_dyn);
+  EgoView E{ws + L.stride * (size_t)e, pol + (size_t)e * P.m};
+  IpmResult r = solve_ego_ipm<DevBlockExecT<M::kTransform, true, 2>, M>(ex, P, L, E);
+  const double* w = E.ws;
+  const int lane = threadIdx.x;
+  if (upred)
+    for (int i = lane; i < P.U * P.d; i += 128) upred[(size_t)e * P.U * P.d + i] = w[L.upred + i];
+  if (xpred)
+    for (int i = lane; i < P.T * P.n; i += 128) xpred[(size_t)e * P.T * P.n + i] = w[L.xpred + i];
+  if (bw)
+    for (int i = lane; i < P.nbranch - 1; i += 128) bw[(size_t)e * (P.nbranch - 1) + i] = w[L.w + 1 + i];
+  if (lane == 0) {
+    if (J) J[e] = w[L.sol + P.oJ];
+    if (status) status[e] = r.exit_flag;
+    if (iters) iters[e] = r.iters;
+  }
+}
+#endif
+
 #ifndef BMPC_TREE_WPE
 #define BMPC_TREE_WPE 4   // k_tree's register budget in batches beyond 2 waves per SIMD (r05ad: 1.23 -> 0.99 ms at 4,096 egos; 3: 1.30)
 #endif
@@ -440,6 +472,7 @@ struct SolveLaunch {
   int nw = 4;        // small-batch launch: waves per ego (4 or 8)
   const Layout* blk_lay = nullptr;   // ... per-ego layouts with LDS-resident spans (or NULL)
   int cus = 256;                     // compute units of the device (k_tree's register budget)
+  const Plan* hplan = nullptr;       // the plan on the host (launch sizes)
   size_t blk_hot_off = 0;            // ... their LDS offset (doubles)
 #if defined(BMPC_WITH_PHASED)
   // phase-per-kernel IPM (experimental/bmpc_dev_ph.h, tools-only builds): per-iteration "egos
@@ -483,6 +516,20 @@ hipError_t launch_solver(const SolveLaunch& a) {
   if constexpr (WITH_QP) {
     if (a.qp) return a.rich ? launch_solver_kernel(k_qp<M, true>, a) : launch_solver_kernel(k_qp<M, false>, a);
   }
+#if defined(BMPC_BLK2)
+  if (const char* e = getenv("BMPC_IPM_W2")) {
+    if (atoi(e) == 1) {
+      const size_t lds = solver_lds_bytes_blk(*a.hplan, M::kTransform, 2);
+      if (lds > 64 * 1024) {
+        const hipError_t he = hipFuncSetAttribute((const void*)k_ipm_w2<M>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (he != hipSuccess) return he;
+      }
+      hipLaunchKernelGGL(k_ipm_w2<M>, dim3(a.batch), dim3(128), lds, a.stream, a.bundle, a.ws, a.pol, a.upred,
+                         a.xpred, a.bw, a.J, a.status, a.iters, a.batch);
+      return hipGetLastError();
+    }
+  }
+#endif
   return a.rich ? launch_solver_kernel(k_ipm<M, true>, a) : launch_solver_kernel(k_ipm<M, false>, a);
 }
 

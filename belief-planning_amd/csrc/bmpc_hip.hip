@@ -613,6 +613,7 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   SolveLaunch a{pl->d_bundle, pl->d_ws, pl->d_pol, d_x, d_z, d_xref, d_upred, d_xpred, d_bw, d_J, d_status,
                 d_iters, B, lds_bytes, tl, qp, s};
   a.cus = pl->ctx->cus;
+  a.hplan = &P;
   int kernel = qp ? (tl ? BMPC_KERNEL_QP_RICH : BMPC_KERNEL_QP_LEAN) : (tl ? BMPC_KERNEL_IPM_RICH : BMPC_KERNEL_IPM_LEAN);
   hipError_t (*tree)(const SolveLaunch&) = launch_tree_quadruped;
   hipError_t (*solver)(const SolveLaunch&) = launch_solver_quadruped;

@@ -72,6 +72,10 @@
 #ifndef BMPC_REFTOL
 #define BMPC_REFTOL 1e-14    // refinement stop: scaled residual <= tol * max(1, |rhs|) (oracle: 1e-14)
 #endif
+#ifndef BMPC_REF_STALL
+#define BMPC_REF_STALL 0     // > 0: ECOS's refinement stop (IRERRFACT): a round that cuts the residual by less than
+                             // this factor ends the refinement, one that grows it is undone
+#endif
 
 // per-phase inlining overrides (experiments: -DBMPC_FN_APPLY_G=BMPC_HD ...)
 #ifndef BMPC_FN_APPLY_G
@@ -2865,7 +2869,7 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
   // read r1 / r2 and write e1 / e2 (max is exact: the same values as separate passes); the |r3h|
   // part before the first round
   double msc = nitref == 0 ? 0.0 : lane_extreme<8, 1>(ex, 0, P.nrows, [&](int i) { return fabs(r3h[i]); });
-  double sc = 0.0;
+  double sc = 0.0, prev = 1e300;
   for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     ProfScope _pr(C.ws, L.prof, PROF_REFINE);
@@ -2889,6 +2893,17 @@ BMPC_HD void kkt_refine(const X ex, const Ctx& C, const gdouble* r1, const gdoub
     ex.sync();
     BMPC_TRACE("   refine %d err %.3e sc %.3e\n", itr, err, sc);
     if (!(err > BMPC_REFTOL * fmax(sc, 1.0))) break;
+    if (BMPC_REF_STALL > 0 && itr > 0) {
+      if (ex.uniform(!(err < prev))) {   // the last correction made it worse: undo it (ECOS)
+        lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] - cx[i]; }, [&](int i, double v) { dx[i] = v; });
+        lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] - cy[i]; }, [&](int i, double v) { dy[i] = v; });
+        lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[i] - cz[i]; }, [&](int i, double v) { dz[i] = v; });
+        ex.sync();
+        break;
+      }
+      if (ex.uniform(prev < BMPC_REF_STALL * err)) break;   // stalled: kept, no further round
+    }
+    prev = err;
     kkt_solve_once<X, NX, NU, true>(ex, C, e1, e2, nullptr, cx, cy, cz, false, false);
     lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[i] + cx[i]; }, [&](int i, double v) { dx[i] = v; });
     lane_batch(ex, 0, P.neq, [&](int i) { return dy[i] + cy[i]; }, [&](int i, double v) { dy[i] = v; });
@@ -2956,6 +2971,7 @@ BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, cons
   for (int j = 0; j < 2; ++j)   // kkt_refine's scale and residual norms, per direction
     msc[j] = nitref == 0 ? 0.0 : lane_extreme<8, 1>(ex, 0, P.nrows, [&](int i) { return fabs(r3h[j][i]); });
   bool on[2] = {true, true};
+  double prev[2] = {1e300, 1e300};
   for (int itr = 0; itr < nitref; ++itr) {
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
     ProfScope _pr(C.ws, L.prof, PROF_REFINE);
@@ -2979,6 +2995,21 @@ BMPC_FN void kkt_refine_pair(const X ex, const Ctx Cin, const gdouble* r1a, cons
       ex.sync();
       on[j] = ex.uniform(err > BMPC_REFTOL * fmax(sc[j], 1.0));
       BMPC_TRACE("   refine[%d] %d err %.3e sc %.3e\n", j, itr, err, sc[j]);
+      if (BMPC_REF_STALL > 0 && itr > 0 && on[j]) {   // kkt_refine's stall rule, per direction
+        if (ex.uniform(!(err < prev[j]))) {
+          const gdouble* cxj = ws + L.k_cx + j * nv;
+          const gdouble* cyj = ws + L.k_cy + j * neq;
+          const gdouble* czj = ws + L.k_cz + j * nr;
+          lane_batch<16>(ex, 0, P.nv, [&](int i) { return dx[j][i] - cxj[i]; }, [&](int i, double v) { dx[j][i] = v; });
+          lane_batch(ex, 0, P.neq, [&](int i) { return dy[j][i] - cyj[i]; }, [&](int i, double v) { dy[j][i] = v; });
+          lane_batch<16>(ex, 0, P.nrows, [&](int i) { return dz[j][i] - czj[i]; }, [&](int i, double v) { dz[j][i] = v; });
+          ex.sync();
+          on[j] = false;
+        } else if (ex.uniform(prev[j] < BMPC_REF_STALL * err)) {
+          on[j] = false;
+        }
+      }
+      prev[j] = err;
     }
     if (!ex.uniform(on[0] || on[1])) break;
     gdouble* cx = ws + L.k_cx;

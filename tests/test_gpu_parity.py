@@ -76,6 +76,29 @@ def test_replay_matches_reference(gpu, name, steps, solver_path):
     np.testing.assert_allclose(ws["jcons"], rb["jcons"])
 
 
+def test_replay_exit_agreement_pooled(gpu, solver_path):
+    """Exit codes of all 184 recorded highway steps (the four loops above) on one launch path:
+    >= 97% agree with the recording.  0 vs 10 is decided at the 1e-8 margin, where the GPU's
+    rounding (FMA contraction, 64-lane reduction trees) and the host build's differ: the traces of
+    the N=10 loop (profiles/r06/trace_*) diverge from 2.6e-13 at iteration 0 and the final primal
+    residual of a step lands anywhere in 1e-10 .. 1.5e-8; the host build with FMA contraction
+    flips 9 of 454 recorded / seeded step decisions the same way (profiles/r06/refine_ab.log)."""
+    agree, total = 0, 0
+    for name, steps in (("highway_n20_nb1", 100), ("highway_n8_nb2", 40), ("highway_n10_nb1", 20),
+                        ("highway_n30_nb2", 24)):
+        g = golden(name)
+        rb = replay_batch(g, steps)
+        pl = gpu.BatchPlan(highway_desc_from_golden(g), rb["T"])
+        pl.set_policies(rb["rows"])
+        pl.set_warm_start(rb["uLin"], rb["p"], rb["jcons"], mask=rb["warm"])
+        r = pl.solve(rb["x"], rb["z"], rb["xref"])
+        assert_solver_path(pl, solver_path)
+        agree += int(np.sum(r["status"] == np.asarray(g["traj_exit"][:rb["T"]])))
+        total += rb["T"]
+    print(f"pooled replay [{solver_path[0]}]: exit codes agree on {agree} of {total} recorded steps")
+    assert total == 184 and agree >= 0.97 * total, (agree, total)
+
+
 def test_batch_matches_host_build(gpu):
     """Seeded batch: every GPU ego equals the host build of the same algorithm."""
     import hostsim_lib as H
@@ -97,10 +120,15 @@ def test_batch_matches_host_build(gpu):
         tight = (r["status"] == 0) & (h["status"] == 0)
         # 0 vs 10 is decided at the rounding floor: which of the egos that stall near 1e-8 make it
         # moves with the summation order (two GPU builds of one algorithm that sum cone rows in
-        # different orders agree on 97.4% of a 4096-ego batch with the same 0/10 split), so the
-        # bar is on the 192 ego-steps of the run, with a looser per-step floor
+        # different orders agree on 97.4% of a 4096-ego batch with the same 0/10 split; the host
+        # build with and without FMA contraction on 186 of these 192 ego-steps, profiles/r06/
+        # refine_ab.log), so the bar is on the 192 ego-steps of the run (>= 95%; round 6: 188), with
+        # a per-step floor of 90% (round 6: 64, 63, 61 of 64)
         agree.append(np.mean(r["status"] == h["status"]))
-        assert agree[-1] >= 0.8, (step, agree)
+        print(f"GPU vs host build, step {step}: exit codes agree on {int(np.sum(r['status'] == h['status']))} of {B}; "
+              f"both exit 0 on {int(tight.sum())}, max |du0| there "
+              f"{np.abs(r['upred'][tight, 0] - h['upred'][tight, 0]).max() if tight.any() else 0:.1e}")
+        assert agree[-1] >= 0.9, (step, agree)
         np.testing.assert_allclose(r["J"][tight], h["J"][tight], rtol=1e-6)
         np.testing.assert_allclose(r["upred"][tight, 0], h["upred"][tight, 0], atol=1e-5)
         np.testing.assert_allclose(r["J"], h["J"], rtol=1e-4)
@@ -108,7 +136,7 @@ def test_batch_matches_host_build(gpu):
         u0 = r["upred"][:, 0]
         x = x + 0.1 * np.stack([x[:, 2] * np.cos(x[:, 3]), x[:, 2] * np.sin(x[:, 3]), u0[:, 0], u0[:, 1]], 1)
         z = z + 0.1 * np.stack([z[:, 2] * np.cos(z[:, 3]), z[:, 2] * np.sin(z[:, 3]), 0 * z[:, 0], 0 * z[:, 0]], 1)
-    assert np.mean(agree) >= 0.9, agree
+    assert np.mean(agree) >= 0.95, agree
 
 
 def _check_sample_against_oracle(r, N, NB, x, z, xref, tgt, egos, workers=None):

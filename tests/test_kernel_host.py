@@ -7,10 +7,12 @@ solves with ECOS to 1e-8 (MPC_branch.py:2136); exit 0 steps must reproduce J to 
 relative and uPred[0] to 1e-6 absolute (observed at most 4.7e-7, on one step of
 the N=30 NB=2 loop, and <= 6e-8 on the others); exit 10 ("inaccurate", ECOS stopped at 1e-4/5e-5)
 steps to 1e-4 relative / 5e-3 absolute -- those optima are only defined that loosely.
-Whether a step ends 0 or 10 is decided at the rounding floor, so exit codes must agree on
-at least 95% of the steps on the host build (90% on the GPU's launch paths) (observed with ECOS's equilibration in the oracle and the kernel,
-round 5: all 20 of highway_n10_nb1, 99 of 100 of n20_nb1, all 40 of n8_nb2; rounds 1-4,
-unequilibrated: 92 of 100 on n20_nb1).  The solver exits by ECOS's rules only -- full accuracy, or reduced accuracy of
+A step the reference solved to full accuracy is held to the tight bars whichever exit the
+kernel returns there.  Whether a step ends 0 or 10 is decided at the rounding floor, so exit
+codes must agree on at least 95% of the steps on the host build (observed with ECOS's
+equilibration in the oracle and the kernel: all 20 of highway_n10_nb1, 99 of 100 of n20_nb1, all
+40 of n8_nb2, all 24 of n30_nb2; rounds 1-4, unequilibrated: 92 of 100 on n20_nb1); on the GPU's
+launch paths at most max(2, 5%) per loop and >= 97% over the 184 steps of the four loops.  The solver exits by ECOS's rules only -- full accuracy, or reduced accuracy of
 the best iterate at maxit / on a failed step; the earlier 5-iteration stall exit is gone (it
 never fired on these scenes nor on a 512-ego seeded batch).
 """
@@ -22,7 +24,12 @@ from common import golden, highway_desc, highway_desc_from_golden, highway_polic
     seeded_batch, unique_mask
 
 
-def check_replay(r, g, T, tree=None, min_agree=0.9):
+def check_replay(r, g, T, tree=None, min_agree=None):
+    """min_agree None (the GPU's launch paths): at most max(2, 5% of the steps) exit codes differ
+    from the recording -- a flip at the 1e-8 margin is one step in 20 on the short N=10 loop; the
+    GPU suite also holds every path to >= 97% over all 184 recorded steps (test_gpu_parity)."""
+    if min_agree is None:
+        min_agree = 1.0 - max(2, int(0.05 * T)) / T
     exits = np.asarray(g["traj_exit"][:T])
     J = np.asarray(g["traj_J"][:T])
     u = np.asarray(g["traj_u"][:T])
@@ -33,13 +40,15 @@ def check_replay(r, g, T, tree=None, min_agree=0.9):
     print(f"replay {g['N']}/{g['NB']}: exit codes agree on {int(np.sum(r['status'] == exits))} of {T} steps "
           f"(exit 10 recorded {int(np.sum(exits == 10))}, got {int(np.sum(r['status'] == 10))}); both exit 0: "
           f"max rel |dJ| {relJ[both0].max() if both0.any() else 0:.1e}, max |du0| {du0[both0].max() if both0.any() else 0:.1e}")
-    # ECOS exit 0 vs 10 is decided at the 1e-8 rounding floor; most steps must agree exactly (the
-    # host build >= 95%; the GPU's summation orders flip 2 of the 20 N=10 steps on the one-wave
-    # kernels, round 5)
+    # ECOS exit 0 vs 10 is decided at the 1e-8 rounding floor: most steps must agree
+    # exactly.  Every step the reference solved to full accuracy is held to J 1e-6: uPred[0] to
+    # 1e-6 where the kernel exits 0 too, to 1e-5 where it returns its best iterate as exit 10 (a
+    # score of ~1.2e-8 on the GPU's flips of the N=10 loop, |du0| 3.6e-6 / 5.1e-6 there); only
+    # recorded exit-10 steps, whose recorded point is itself ECOS's reduced-accuracy one, get the
+    # loose bars (1e-4 / 5e-3)
     assert np.mean(r["status"] == exits) >= min_agree, (r["status"], exits)
     for t in range(T):
-        tight = exits[t] == 0 and r["status"][t] == 0
-        rtol, atol = (1e-6, 1e-6) if tight else (1e-4, 5e-3)
+        rtol, atol = ((1e-6, 1e-6) if r["status"][t] == 0 else (1e-6, 1e-5)) if exits[t] == 0 else (1e-4, 5e-3)
         assert abs(r["J"][t] - J[t]) <= rtol * max(1.0, abs(J[t])), (t, exits[t], r["J"][t], J[t])
         np.testing.assert_allclose(r["upred"][t, 0], u[t], atol=atol, err_msg=f"step {t}")
     if tree is not None:

@@ -37,8 +37,11 @@ def xform_desc(g):
     return d
 
 
-def replay(solver, g, steps):
-    """Drive a HostSim / BatchPlan (batch 1) through the recorded steps with the schedule."""
+def replay(solver, g, steps, recorded_ws=False):
+    """Drive a HostSim / BatchPlan (batch 1) through the recorded steps with the schedule.
+    recorded_ws: hand every step after the first the warm start the reference carried into it
+    (checkpoint ABI; the state rows in force still follow the solver's own argument history),
+    so each step's problem is the reference's -- otherwise the solver carries its own."""
     out = dict(status=[], J=[], u0=[], dp=[])
     last_tgt = None
     for t in range(steps):
@@ -46,6 +49,8 @@ def replay(solver, g, steps):
         if tgt != last_tgt:
             solver.set_policies(highway_policy_rows([tgt], float(g["Kpsi"])))
             last_tgt = tgt
+        if recorded_ws and t > 0:
+            solver.set_warm_start(np.asarray(g["traj_ws_uLin"][t])[None], np.asarray(g["traj_ws_p"][t])[None])
         S, Fx, bx = schedule(g, t)
         if Fx is not None:
             solver.set_fx(np.asarray(Fx)[None])
@@ -58,20 +63,32 @@ def replay(solver, g, steps):
     return {k: np.array(v) for k, v in out.items()}
 
 
-def check_replay(out, g, steps):
+def check_replay(out, g, steps, u_tol=1e-6, dp_tol=1e-6, tag=""):
+    """Exit codes, J (1e-6 relative), uPred[0] (u_tol) and the live tree's dp (root branch 1e-12,
+    the others dp_tol) against the recording."""
     ex = np.asarray(g["traj_exit"][:steps])
     assert np.all(out["status"] >= 0), out["status"]
-    assert np.mean(out["status"] == ex) >= 0.9, (out["status"], ex)
     both = (out["status"] == 0) & (ex == 0)
     Jr = np.asarray(g["traj_J"][:steps])
-    np.testing.assert_allclose(out["J"][both], Jr[both], rtol=1e-6)
-    # (the solver carries its own warm start from step to step, so differences at the rounding
-    # floor accumulate along the 18 steps: observed 2.2e-6 on the host build, 1.9e-5 on the GPU's
-    # 4-wave kernel, round 5)
-    np.testing.assert_allclose(out["u0"][both], np.asarray(g["traj_u"][:steps])[both], atol=3e-5)
+    du = np.abs(out["u0"] - np.asarray(g["traj_u"][:steps])).max(axis=1)
     dpr = np.asarray(g["traj_dp"][:steps])
+    print(f"xform replay{tag}: exit codes agree on {int(np.sum(out['status'] == ex))} of {steps} steps; max |du0| "
+          f"{du[both].max():.1e} (per step {' '.join(f'{v:.0e}' for v in du)}); max |ddp| {np.abs(out['dp'] - dpr).max():.1e}")
+    assert np.mean(out["status"] == ex) >= 0.95, (out["status"], ex)
+    np.testing.assert_allclose(out["J"][both], Jr[both], rtol=1e-6)
+    np.testing.assert_allclose(out["u0"][both], np.asarray(g["traj_u"][:steps])[both], atol=u_tol)
     np.testing.assert_allclose(out["dp"][:, 0], dpr[:, 0], rtol=1e-12, atol=1e-12)   # root branch
-    np.testing.assert_allclose(out["dp"], dpr, atol=3e-5)   # (on the carried linearisation: host 1.2e-6)
+    np.testing.assert_allclose(out["dp"], dpr, atol=dp_tol)
+
+
+# The free-running loop (the solver carries its OWN warm start from step to step, as the drop-in
+# does) compounds rounding-floor differences of each solution into the next step's linearisation:
+# observed 2.2e-6 in uPred[0] and 1.2e-6 in dp on the host build, 1.9e-5 on the GPU's 4-wave kernel
+# (round 5).  Handed the reference's own warm start on every step (recorded_ws), each step's problem
+# is the reference's and the same kernels agree to <= 5e-8 (host build; round 6) -- the free-running
+# drift is the loop's amplification of rounding, not a per-step difference, so the per-step replays
+# carry the tight bars and the free-running ones the loop's.
+FREE_U_TOL, FREE_DP_TOL = 3e-5, 3e-5
 
 
 def test_fixture_exercises_the_schedule():
@@ -124,12 +141,13 @@ def test_oracle_restates_reference_rows():
 
 
 def test_host_build_replays_xform_scene():
-    """The kernel templates (host build) replay the whole recording."""
+    """The kernel templates (host build) replay the whole recording: every step with the
+    reference's warm start at the tight bars, and the free-running loop (own warm start)."""
     import hostsim_lib as H
     g = golden(NAME)
     steps = len(g["traj_x"])
-    hs = H.HostSim(xform_desc(g), 1)
-    check_replay(replay(hs, g, steps), g, steps)
+    check_replay(replay(H.HostSim(xform_desc(g), 1), g, steps, recorded_ws=True), g, steps, tag=" (recorded ws)")
+    check_replay(replay(H.HostSim(xform_desc(g), 1), g, steps), g, steps, 5e-6, 5e-6, tag=" (own ws)")
 
 
 def test_host_build_sticky_rows_matter():
@@ -165,7 +183,10 @@ def test_gpu_replays_xform_scene(solver_path):
     steps = len(g["traj_x"])
     from conftest import assert_solver_path
     pl = plan.BatchPlan(xform_desc(g), 1)
-    check_replay(replay(pl, g, steps), g, steps)
+    check_replay(replay(pl, g, steps, recorded_ws=True), g, steps, tag=" (recorded ws)")
+    assert_solver_path(pl, solver_path)
+    pl = plan.BatchPlan(xform_desc(g), 1)
+    check_replay(replay(pl, g, steps), g, steps, FREE_U_TOL, FREE_DP_TOL, tag=" (own ws)")
     assert_solver_path(pl, solver_path)
 
 
@@ -197,6 +218,6 @@ def test_gpu_compat_controller_takes_fx_and_s():
         mpc.solve(g["traj_x"][t], g["traj_z"][t], g["traj_xRef"][t], S=S, Fx=Fx, bx=bx)
         if mpc.status == 0 and g["traj_exit"][t] == 0:
             assert abs(mpc.J - g["traj_J"][t]) <= 1e-6 * abs(g["traj_J"][t]), t
-            np.testing.assert_allclose(mpc.uPred[0], g["traj_u"][t], atol=3e-5)   # (own warm start: see check_replay)
+            np.testing.assert_allclose(mpc.uPred[0], g["traj_u"][t], atol=FREE_U_TOL)   # (own warm start: see check_replay)
         np.testing.assert_allclose(mpc.BT.dp, g["traj_dp"][t][0], rtol=1e-12, atol=1e-12)
         assert mpc.BT.children[0].dp.shape == (3, 4)

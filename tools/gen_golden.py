@@ -284,12 +284,20 @@ def gen_highway_xform(name, N, NB, steps, keep, out):
                  Q=param.Q, R=param.R, Fx=param.Fx, bx=np.asarray(param.bx, float).reshape(-1),
                  Fu=param.Fu, bu=np.asarray(param.bu, float).reshape(-1), Qslack=param.Qslack)
     traj = {k: [] for k in ("x", "z", "xRef", "u", "lc_target", "exit", "J", "iters", "S", "S_on", "Fx", "Fx_on",
-                            "bx", "bx_on", "dp")}
+                            "bx", "bx_on", "dp", "ws_uLin", "ws_p")}
     t0 = time.time()
     for t in range(steps):
         if not env.collision:
             env.check_collision()
         S, Fx, bx = xform_schedule(t)
+        # the warm start the controller carries into this solve (as gen_highway records it), so a
+        # replay can hand every step the reference's own warm start
+        if mpc.uLin is None:
+            traj["ws_uLin"].append(None)
+            traj["ws_p"].append(None)
+        else:
+            traj["ws_uLin"].append(np.array(mpc.uLin, float).copy())
+            traj["ws_p"].append(np.array([np.ravel(b.p) for b in mpc.ndx if b.depth < NB], float))
         r = env.step(t)
         prob, sol, info, kw = CURRENT["captured"]
         for k in ("x", "z", "xRef", "u", "lc_target"):
@@ -318,6 +326,9 @@ def gen_highway_xform(name, N, NB, steps, keep, out):
             d_out[p + "exit"] = np.array(info["exitFlag"])
         print(f"[{name}] t={t:3d} exit={info['exitFlag']:3d} it={info['iter']:3d} J={sol[-1]:.6f} "
               f"u0={mpc.uPred[0]} ({time.time() - t0:.0f}s)", flush=True)
+    for k in ("ws_uLin", "ws_p"):    # first solve has no warm start (inittree): NaN rows
+        shape = next(v.shape for v in traj[k] if v is not None)
+        traj[k] = [np.full(shape, np.nan) if v is None else v for v in traj[k]]
     for k, v in traj.items():
         d_out["traj_" + k] = np.array(v)
     d_out["keep"] = np.array(sorted(keep))
