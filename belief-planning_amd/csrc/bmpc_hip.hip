@@ -580,7 +580,15 @@ static int blk_layouts(bmpc_plan* pl, size_t lds_base) {
         if (f0[i] >= a && f0[i] < b) f[i] = (size_t)((int64_t)f0[i] + delta);
     }
   }
-  if (!pl->d_blk_lay) HIPCHECK(hipMalloc(&pl->d_blk_lay, sizeof(Layout) * (size_t)B));
+  if (!pl->d_blk_lay) {
+    HIPCHECK(hipMalloc(&pl->d_blk_lay, sizeof(Layout) * (size_t)B));
+  } else {
+    // a rebuild (the launch's LDS base changed, e.g. BMPC_BLOCK_WAVES toggled between solves):
+    // a small-batch kernel still in flight on the plan's or the caller's stream reads the old
+    // layouts -- let those streams drain before the buffer is overwritten
+    HIPCHECK(hipStreamSynchronize(pl->stream));
+    if (pl->user_stream) HIPCHECK(hipStreamSynchronize(pl->user_stream));
+  }
   HIPCHECK(hipMemcpy(pl->d_blk_lay, lays.data(), sizeof(Layout) * (size_t)B, hipMemcpyHostToDevice));
   pl->blk_lay_base = lds_base;
   pl->blk_hot_off = at[0];
@@ -719,6 +727,7 @@ int bmpc_solve_device(bmpc_plan* pl, const double* d_x, const double* d_z, const
   if (!pl || !d_x || !d_z || !d_xref) return fail(-22, "null argument");
   HIPCHECK(hipSetDevice(pl->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
+  if (stream) pl->user_stream = s;   // (synchronised before the plan's device state is rewritten)
   return launch_solve(pl, d_x, d_z, d_xref, d_upred, d_xpred, d_branch_w, d_J, d_status, d_iters, s);
 }
 

@@ -39,14 +39,15 @@ from bmpc.scenarios import (LANES, highway_desc, highway_desc_from_golden, highw
                             seeded_batch, xref_rule)
 
 
-def unique_mask(T, NB, N, m, Nc=5, n=4, d=2):
+def unique_mask(T, NB, N, m, Nc=5, n=4, d=2, nb2_aux=True):
     """Solution entries that are unique at the optimum: everything except the slacks of the
     leaf terminal nodes, which appear in no cost and no constraint but -S <= 0
-    (MPC_branch.py:1886-1892 only fills rows i < len(utraj); SURVEY quirk register), and, on
-    NB = 2 trees, the CVaR auxiliaries (rho, sigma, mu+, mu-; MPC_branch.py:1752-1804, 1940-1967):
-    there the interior point's choice moves along a flat direction of them at the rounding floor
-    (N=30 NB=2, step 1: the same 3e-4 relative difference on six mu entries of one branch point,
-    every other entry <= 1e-10)."""
+    (MPC_branch.py:1886-1892 only fills rows i < len(utraj); SURVEY quirk register).  On NB = 2
+    trees the CVaR auxiliaries sigma, mu+, mu- (MPC_branch.py:1752-1804, 1940-1967) sit on a
+    nearly flat direction: the interior point's choice moves along it at the rounding floor (host
+    build vs recordings, kept steps: rho <= 4e-9, sigma <= 2.6e-5, mu+ <= 3.3e-4, mu- <= 3.7e-5
+    relative), inside the callers' 1e-3 bar, so they stay in the comparison (nb2_aux=False drops
+    them)."""
     from oracle.tree import Topology
     t = Topology.build(N, NB, m)
     bd = t.bdim
@@ -54,8 +55,8 @@ def unique_mask(T, NB, N, m, Nc=5, n=4, d=2):
     oS = oRho + bd * (2 * m + 2)
     nv = oS + T * Nc + 1
     mask = np.ones(nv, bool)
-    if NB >= 2:
-        mask[oRho:oS] = False
+    if NB >= 2 and not nb2_aux:
+        mask[oRho + bd:oS] = False
     for b in range(t.nbranch):
         if t.is_leaf(b):
             k = t.ndx[b] + N
