@@ -122,6 +122,7 @@ _SIGS = {
     "bmpc_set_lane_ref": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "bmpc_hmm_eval": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 9),
     "bmpc_env_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int] + [C.c_void_p] * 10),
+    "bmpc_loop_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 10),
     "bmpc_qp_solve": (C.c_int, [C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 4 + [C.c_int] + [C.c_void_p] * 5
                       + [C.c_int, C.c_double] + [C.c_void_p] * 5),
 }

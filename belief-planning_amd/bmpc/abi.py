@@ -19,7 +19,7 @@ MAX_LANE_REF = 4096
  INFO_LP, INFO_BATCH, INFO_WS_DOUBLES, INFO_SOLVER, INFO_COUNT) = range(13)
 # solver kernels reported in INFO_SOLVER (include/bmpc.h BMPC_KERNEL_*)
 (KERNEL_NONE, KERNEL_IPM_RICH, KERNEL_IPM_LEAN, KERNEL_IPM_BLK4, KERNEL_IPM_BLK8, KERNEL_QP_RICH,
- KERNEL_QP_LEAN) = range(7)
+ KERNEL_QP_LEAN, KERNEL_LOOP_RICH, KERNEL_LOOP_LEAN) = range(9)
 
 
 class Policy(C.Structure):

@@ -103,6 +103,15 @@ class BatchPlan:
                                                      x_ptr, z_ptr, xref_ptr, stats_ptr, stream)]
         check(lib().bmpc_env_step(self._h, C.byref(env), int(t), *vp), "bmpc_env_step")
 
+    def loop_device(self, env: abi.EnvDesc, t0: int, nsteps: int, scene_ptr, upred_ptr, x_ptr, z_ptr, xref_ptr,
+                    J_ptr, status_ptr, iters_ptr, stats_ptr=None, stream=None):
+        """nsteps closed-loop steps of every ego (bmpc_loop_device): env_step_device(t) then
+        solve_device for t = t0 .. t0+nsteps-1, the same results; one fused launch (k_loop) when
+        the batch takes the one-wave IPM.  Async on `stream`."""
+        vp = [C.c_void_p(p) if p else None for p in (scene_ptr, upred_ptr, x_ptr, z_ptr, xref_ptr, J_ptr, status_ptr,
+                                                     iters_ptr, stats_ptr, stream)]
+        check(lib().bmpc_loop_device(self._h, C.byref(env), int(t0), int(nsteps), *vp), "bmpc_loop_device")
+
     def get_warm_start(self):
         """Checkpoint of the per-ego warm start (uLin, p, Jcons, OldInput)."""
         B, d = self.batch, self.desc.d

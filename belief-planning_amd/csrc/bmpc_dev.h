@@ -486,6 +486,69 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) 
   }
 }
 
+// The three parts of a k_loop step as calls of their own: each gets its registers allocated
+// apart from the others' (the scene step's and the tree step's private arrays and live values
+// stay out of the IPM loop's 128-VGPR budget).
+template <class X, class M>
+__device__ __attribute__((noinline)) void loop_tree_step(const X ex, const Plan& P, const Layout& L, EgoView E,
+                                                          const double* x, const double* z, const double* xref) {
+  tree_step<X, M>(ex, P, L, E, x, z, xref);
+}
+template <class X, class M>
+__device__ __attribute__((noinline)) IpmResult loop_ipm(const X ex, const Plan& P, const Layout& L, EgoView E) {
+  return solve_ego_ipm<X, M>(ex, P, L, E);
+}
+__device__ __attribute__((noinline)) void loop_env_step(const bmpc_env_desc& env, double dt, int N, int m, int t,
+                                                        double* st, bmpc_policy* pol, const double* up, double* x,
+                                                        double* z, double* xr, double Jv, int status, int iters,
+                                                        double* stats) {
+  if (t > 0 && stats) env_accumulate(st, Jv, status, iters, true, stats);
+  env_step_ego(env, dt, N, m, t, st, pol, up, x, z, xr);
+}
+
+// nsteps closed-loop steps of one ego per wave (bmpc_loop_device): k_env's scene step (lane 0),
+// k_tree's tree step and k_ipm's solve + unpack, in that order, per step -- the same per-ego
+// functions the three launches run, so the same bits -- with no device-wide boundary between
+// the steps: the egos' loops are independent, and a wave whose ego needs few IPM iterations in
+// one step starts its next step instead of idling until the slowest ego of the batch finishes.
+template <class M, bool TL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BMPC_WPE))) void k_loop(
+    const Bundle* __restrict__ B, double* __restrict__ ws, bmpc_policy* __restrict__ pol, bmpc_env_desc env, int t0,
+    int nsteps, double* scene, double* upred, double* xs, double* zs, double* xrefs, double* J, int32_t* status,
+    int32_t* iters, double* stats, int batch) {
+  const int e = blockIdx.x;
+  if (e >= batch) return;
+  const Plan& P = B->P;
+  const Layout& L = B->L;
+  extern __shared__ double lds_dyn[];
+  const auto ex = solver_exec<M::kTransform, TL>(P, lds_dyn);
+  bmpc_policy* pe = pol + (size_t)e * P.m;
+  EgoView E{ws + L.stride * (size_t)e, pe};
+  double* st = scene + (size_t)e * ENV_STRIDE;
+  double* up = upred + (size_t)e * P.U * P.d;
+  double* x = xs + (size_t)e * P.n;
+  double* z = zs + (size_t)e * P.n;
+  double* xr = xrefs + (size_t)e * P.n;
+  const int lane = threadIdx.x;
+  for (int s = 0; s < nsteps; ++s) {
+    const int t = t0 + s;
+    if (lane == 0)   // k_env
+      loop_env_step(env, P.desc.dt, P.N, P.m, t, st, pe, up, x, z, xr, J[e], status[e], iters[e],
+                    stats ? stats + (size_t)e * ENVS_STRIDE : nullptr);
+    __syncthreads();
+    loop_tree_step<DevExecT<M::kTransform, TL>, M>(ex, P, L, E, x, z, xr);   // k_tree
+    const IpmResult r = loop_ipm<DevExecT<M::kTransform, TL>, M>(ex, P, L, E);   // k_ipm
+    const double* w = E.ws;
+    for (int i = lane; i < P.U * P.d; i += 64) up[i] = w[L.upred + i];
+    if (lane == 0) {
+      J[e] = w[L.sol + P.oJ];
+      status[e] = r.exit_flag;
+      iters[e] = r.iters;
+    }
+    __syncthreads();
+  }
+}
+
 // one solve launch of a plan (device pointers; the timing events are recorded by the caller
 // between the two launches)
 struct SolveLaunch {
@@ -564,6 +627,22 @@ hipError_t launch_solver(const SolveLaunch& a) {
   return a.rich ? launch_solver_kernel(k_ipm<M, true>, a) : launch_solver_kernel(k_ipm<M, false>, a);
 }
 
+// the fused closed loop (k_loop): the one-wave IPM's LDS and register budget
+template <class M>
+hipError_t launch_loop(const SolveLaunch& a, const bmpc_env_desc& env, int t0, int nsteps, double* scene,
+                       double* stats) {
+  void (*k)(const Bundle*, double*, bmpc_policy*, bmpc_env_desc, int, int, double*, double*, double*, double*,
+            double*, double*, int32_t*, int32_t*, double*, int) = a.rich ? k_loop<M, true> : k_loop<M, false>;
+  if (a.lds_bytes > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)a.lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(a.batch), dim3(64), a.lds_bytes, a.stream, a.bundle, a.ws, const_cast<bmpc_policy*>(a.pol),
+                     env, t0, nsteps, scene, a.upred, const_cast<double*>(a.x), const_cast<double*>(a.z),
+                     const_cast<double*>(a.xref), a.J, a.status, a.iters, stats, a.batch);
+  return hipGetLastError();
+}
+
 // the small-batch launch: one ego per NW-wave workgroup (solver_lds_bytes_blk of LDS)
 template <class M, bool QP, int NW>
 hipError_t launch_blk_kernel(const SolveLaunch& a) {
@@ -602,6 +681,8 @@ hipError_t launch_solver_blk_highway(const SolveLaunch& a);
 hipError_t launch_solver_blk_highway_t(const SolveLaunch& a);
 hipError_t launch_solver_blk_merge(const SolveLaunch& a);
 hipError_t launch_solver_blk_quadruped(const SolveLaunch& a);
+hipError_t launch_loop_highway(const SolveLaunch& a, const bmpc_env_desc& env, int t0, int nsteps, double* scene,
+                               double* stats);
 #if defined(BMPC_WITH_PHASED)
 // the phase-per-kernel CVaR IPM (experimental/bmpc_kp_*.hip; tools-only builds with -DBMPC_WITH_PHASED)
 hipError_t launch_ipm_phased_highway(const SolveLaunch& a);

@@ -751,6 +751,59 @@ int bmpc_env_step(bmpc_plan* pl, const bmpc_env_desc* env, int t, double* d_scen
   return 0;
 }
 
+// nsteps closed-loop steps (include/bmpc.h): one k_loop launch for CVaR batches that take the
+// one-wave IPM, otherwise bmpc_env_step + the solve launches per step (same results either way)
+int bmpc_loop_device(bmpc_plan* pl, const bmpc_env_desc* env, int t0, int nsteps, double* d_scene, double* d_upred,
+                     double* d_x, double* d_z, double* d_xref, double* d_J, int32_t* d_status, int32_t* d_iters,
+                     double* d_stats, void* stream) {
+  if (!pl || !env || !d_scene || !d_upred || !d_x || !d_z || !d_xref || !d_J || !d_status || !d_iters)
+    return fail(-22, "null argument");
+  const Plan& P = pl->hp.plan;
+  if (P.desc.model != BMPC_MODEL_HIGHWAY || (P.desc.flags & BMPC_PLAN_TRANSFORM) || P.n != 4 || P.d != 2)
+    return fail(-22, "bmpc_loop_device: the overtake scene needs a highway plan (n = 4, d = 2) without transform");
+  if (P.desc.controller != BMPC_CTRL_CVAR && P.desc.controller != BMPC_CTRL_ROBUST)
+    return fail(-22, "bmpc_loop_device: CVaR or robust controllers only");
+  if (nsteps < 1 || t0 < 0) return fail(-22, "bmpc_loop_device: nsteps >= 1 and t0 >= 0");
+  if (env->n_lane < 1) return fail(-22, "bmpc_loop_device: n_lane < 1");
+  HIPCHECK(hipSetDevice(pl->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : pl->stream;
+  if (stream) pl->user_stream = s;
+  const int B = pl->batch;
+  int blk_max = pl->ctx->cus;   // the small-batch path of launch_solve
+  if (const char* e = getenv("BMPC_BLOCK_EGOS")) blk_max = atoi(e);
+  bool fused = P.desc.controller == BMPC_CTRL_CVAR && B > blk_max && !pl->psiref;
+  if (const char* e = getenv("BMPC_LOOP_FUSED")) fused = fused && atoi(e) != 0;   // 0: per-step launches (A/B)
+  if (!fused) {
+    for (int k = 0; k < nsteps; ++k) {
+      if (int rc = bmpc_env_step(pl, env, t0 + k, d_scene, d_upred, d_J, d_status, d_iters, d_x, d_z, d_xref, d_stats,
+                                 stream))
+        return rc;
+      if (int rc = launch_solve(pl, d_x, d_z, d_xref, d_upred, nullptr, nullptr, d_J, d_status, d_iters, s)) return rc;
+    }
+    return 0;
+  }
+  if (pl->timing && (pl->t_pending < 0 || pl->t_pending >= bmpc_plan::kTimeSlots))
+    return fail(-5, "timing ring out of range (t_pending = " + std::to_string(pl->t_pending) + ")");
+  const bool tl = choose_lds_rich(P, false, B, pl->ctx->cus, pl->ctx->lds_per_cu);
+  SolveLaunch a{pl->d_bundle, pl->d_ws, pl->d_pol, d_x, d_z, d_xref, d_upred, nullptr, nullptr, d_J, d_status,
+                d_iters, B, solver_lds_bytes(P, false, tl), tl, false, s};
+  a.cus = pl->ctx->cus;
+  a.hplan = &P;
+  pl->last_kernel = tl ? BMPC_KERNEL_LOOP_RICH : BMPC_KERNEL_LOOP_LEAN;
+  hipEvent_t* ev = pl->ev + 3 * (pl->timing ? pl->t_pending : 0);
+  if (pl->timing) {   // (the whole fused launch is booked as the solver's time, none as the tree's)
+    HIPCHECK(hipEventRecord(ev[0], s));
+    HIPCHECK(hipEventRecord(ev[1], s));
+  }
+  HIPCHECK(launch_loop_highway(a, *env, t0, nsteps, d_scene, d_stats));
+  pl->pol_on_device = true;
+  if (pl->timing) {
+    HIPCHECK(hipEventRecord(ev[2], s));
+    if (++pl->t_pending == bmpc_plan::kTimeSlots) return fold_timing(pl);
+  }
+  return 0;
+}
+
 static int gather(bmpc_plan* pl, size_t off, int count, double* host) {
   if (!host) return 0;
   const size_t need = (size_t)pl->batch * count;

@@ -227,6 +227,10 @@ def main():
                     help="egos over all ranks, sharded contiguously (BASELINE config 5: 65536 over 8 GPUs)")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--NB", type=int, default=None)
+    ap.add_argument("--loop", choices=("fused", "steps"), default="steps",
+                    help="highway CVaR closed loop: fused = the K steps of every ego in one k_loop launch "
+                         "(bmpc_loop_device: the egos' loops are independent, so no step waits for the slowest "
+                         "ego of the previous one); steps = k_env + k_tree + k_ipm launched per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-egos", type=int, default=4096, help="egos of the C++ host-build baseline sample")
     ap.add_argument("--oracle-egos", type=int, default=16, help="egos of the NumPy-oracle baseline sample")
@@ -338,6 +342,15 @@ def main():
         estats[:, abi.ENVS_SOLVES] += 1.0
         estats[:, abi.ENVS_COLL_STEPS] += (dis < 0).double()
 
+    fused = a.loop == "fused" and not (quad or robust or host)
+
+    def steps(k):
+        """k closed-loop steps of every ego as ONE launch (bmpc_loop_device -> k_loop), the same
+        per-ego work and results as k calls of step()"""
+        pl.loop_device(env, tstep[0], k, scene.data_ptr(), up.data_ptr(), tx.data_ptr(), tz.data_ptr(), tr.data_ptr(),
+                       Jv.data_ptr(), st.data_ptr(), it.data_ptr(), estats.data_ptr(), sh)
+        tstep[0] += k
+
     def step():
         # one closed-loop step: scene update -> solve (inputs / outputs stay in HBM)
         if not quad:
@@ -351,9 +364,13 @@ def main():
             quad_env_step()
 
     it_sum = torch.zeros(B, dtype=torch.float64, device=dev)
-    for _ in range(a.warmup):
-        step()
-        it_sum.add_(it)
+    if fused:
+        if a.warmup:
+            steps(a.warmup)
+    else:
+        for _ in range(a.warmup):
+            step()
+            it_sum.add_(it)
     # the timed region's own torch ops once beforehand: their kernels load lazily on first use
     # (~20-60 ms each, measured at one ego: 2.3 ms per step of a 20-step region)
     D.episode_stats(estats)
@@ -368,9 +385,12 @@ def main():
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        it_sum.add_(it)
+    if fused:
+        steps(a.steps)
+    else:
+        for _ in range(a.steps):
+            step()
+            it_sum.add_(it)
     stats = D.episode_stats(estats)
     D.reduce_stats(stats)        # the only collective: SUM, MAX for the flag
     sync()
@@ -379,8 +399,13 @@ def main():
     elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
     tm = pl.timing()
     pl.enable_timing(False)
-    ipm_ms = D.max_over_ranks(tm["ipm_ms"], device=dev)
-    iters_mean = float(it_sum.sum().item()) / (B * max(a.steps, 1))
+    # per-step kernel time: a fused launch covers a.steps steps (k_env + k_tree + k_ipm work of each)
+    ipm_ms = D.max_over_ranks(tm["ipm_ms"] / (a.steps if fused else 1), device=dev)
+    if fused:   # the closed-loop statistics count every solve's iterations (k_env's accumulate)
+        st_loc = estats.sum(0).cpu().numpy()
+        iters_mean = float(st_loc[abi.ENVS_ITERS] / max(st_loc[abi.ENVS_SOLVES], 1))
+    else:
+        iters_mean = float(it_sum.sum().item()) / (B * max(a.steps, 1))
     total = G * a.steps
     value = total / elapsed
     if rank == 0:
@@ -400,11 +425,13 @@ def main():
         achieved = B * iters_mean * F_it / kern_s / 1e12 if kern_s > 0 else 0.0
         abytes = algorithmic_bytes(T, U, bdim, nbr, desc.m, desc.n, desc.d)
         hbm_alg = B * abytes / kern_s / 1e9 if kern_s > 0 else 0.0
-        key = f"{a.workload}:N{a.N}:NB{a.NB}:B{B}"
+        key = f"{a.workload}:N{a.N}:NB{a.NB}:B{B}" + (":loop" if fused else "")   # traffic per step
         src = _lib.source_hash()
         lib_stamp = None if host else _lib.LOADED_STAMP   # lib() refused the product .so unless == src
         traffic, tsrc = load_traffic(a.traffic, key, src)
-        kname = "k_qp (structured Mehrotra QP IPM)" if (quad or robust) else "k_ipm (structured HSDE IPM)"
+        kname = ("k_qp (structured Mehrotra QP IPM)" if (quad or robust) else
+                 "k_loop (per ego: k_env scene step + k_tree + k_ipm structured HSDE IPM, fused over the steps)"
+                 if fused else "k_ipm (structured HSDE IPM)")
         headline = not (quad or robust) and (a.N, a.NB, B) == (20, 1, 4096)
         out = {
             "metric": (METRIC if headline else
@@ -425,6 +452,8 @@ def main():
                                     f"highway BranchMPC_CVaR closed loop, N={a.N}, NB={a.NB}, m=3 ")
                                    + f"(T={T}, U={U}), {B} egos per GPU", "batch_per_gpu": B,
                        "global_batch": G, "world_size": world, "parallelism": f"ego-sharded dp{world}",
+                       "loop": ("fused: one k_loop launch per timed region (bmpc_loop_device)" if fused else
+                                "per step: k_env + solve launches"),
                        "shards": [list(D.shard(G, r, world)) for r in range(world)]},
             "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 7),

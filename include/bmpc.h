@@ -170,7 +170,9 @@ enum {
   BMPC_KERNEL_IPM_BLK4 = 3,  /* k_solve_blk, one ego per 4-wave workgroup (small batches)  */
   BMPC_KERNEL_IPM_BLK8 = 4,  /* k_solve_blk, one ego per 8-wave workgroup (small batches)  */
   BMPC_KERNEL_QP_RICH = 5,   /* k_qp (OSQP-class controllers), LDS-rich                    */
-  BMPC_KERNEL_QP_LEAN = 6    /* k_qp, lean                                                 */
+  BMPC_KERNEL_QP_LEAN = 6,   /* k_qp, lean                                                 */
+  BMPC_KERNEL_LOOP_RICH = 7, /* k_loop (bmpc_loop_device): env + tree + IPM steps per ego    */
+  BMPC_KERNEL_LOOP_LEAN = 8  /* k_loop, lean                                                 */
 };
 
 const char* bmpc_last_error(void);
@@ -326,6 +328,21 @@ int bmpc_env_step(bmpc_plan* plan, const bmpc_env_desc* env, int t, double* d_sc
                   const double* d_upred, const double* d_J, const int32_t* d_status,
                   const int32_t* d_iters, double* d_x, double* d_z, double* d_xref,
                   double* d_stats, void* stream);
+
+/* nsteps closed-loop steps t0 .. t0+nsteps-1 of every ego, each bmpc_env_step(t) followed by
+ * bmpc_solve_device -- the loop main_branch.sim_overtake runs per ego (Highway_sim,
+ * Highway_env_branch.py:408-436: env.step -> controller solve, repeated) -- with the same
+ * arguments and the same per-ego results, bit for bit.  The egos' loops are independent, so a
+ * CVaR plan whose batch takes the one-wave IPM runs them in ONE launch (k_loop: each wave
+ * steps its ego through all nsteps without a device-wide boundary between steps, so no step
+ * waits for the slowest ego of the previous one); other batches run the two launches per step.
+ * d_upred / d_J / d_status / d_iters hold the last solve's outputs on return (the next call's
+ * t0 > 0 reads them); d_x / d_z / d_xref the last step's solve inputs.  Highway CVaR / robust
+ * plans without transform (the scene's model); -22 otherwise.  An extension of the drop-in ABI
+ * for Monte-Carlo closed-loop batches (BASELINE config 5); the reference has no batched loop. */
+int bmpc_loop_device(bmpc_plan* plan, const bmpc_env_desc* env, int t0, int nsteps, double* d_scene,
+                     double* d_upred, double* d_x, double* d_z, double* d_xref, double* d_J,
+                     int32_t* d_status, int32_t* d_iters, double* d_stats, void* stream);
 
 /* HMM belief-augmented linearisation, batched over B points: replaces
  * HMM_backup_dyn.PredictiveModel.regressionAndLinearization (HMM_backup_dyn.py:216-237) of

@@ -18,7 +18,7 @@ def rows(path):
 
 
 def short(name):
-    for k in ("k_ipm", "k_tree", "k_gather", "k_scatter", "k_reset", "k_model"):
+    for k in ("k_ipm", "k_tree", "k_loop", "k_gather", "k_scatter", "k_reset", "k_model"):
         if k in name:
             return k
     return name[:60]
@@ -58,16 +58,30 @@ def main(out):
             vs = list(per.values())
             agg[k][c] = {"dispatches": len(vs), "avg_per_dispatch": sum(vs) / len(vs)}
     summ["pmc"] = agg
+    # the fused closed loop (bench.py --loop fused): one k_loop dispatch per region; the last
+    # dispatch is the timed one, LOOP_STEPS steps long -- per-step figures from it
+    loop_steps = int(os.environ.get("LOOP_STEPS", "20"))
+    if "k_loop" in pmc:
+        for c, vals in pmc["k_loop"].items():
+            per = defaultdict(float)
+            for d, v in vals:
+                per[int(d)] += v
+            last = per[max(per)]
+            agg["k_loop"][c]["timed_dispatch_per_step"] = last / loop_steps
+        kd = summ.get("kernel_durations_ns", {}).get("k_loop")
+        if kd:
+            kd["timed_dispatch_per_step"] = kd["max"] / loop_steps
     with open(os.path.join(out, "summary.json"), "w") as f:
         json.dump(summ, f, indent=1)
     # per-launch HBM bytes of the IPM kernel (the figure bench.py reports as roofline.traffic)
-    for k in ("k_ipm", "k_qp"):
+    for k in ("k_ipm", "k_qp", "k_loop"):
         a = agg.get(k, {})
         if "FETCH_SIZE" in a and "WRITE_SIZE" in a:
-            fk = a["FETCH_SIZE"]["avg_per_dispatch"]
-            wk = a["WRITE_SIZE"]["avg_per_dispatch"]
+            sel = "timed_dispatch_per_step" if k == "k_loop" else "avg_per_dispatch"   # k_loop: per step
+            fk = a["FETCH_SIZE"][sel]
+            wk = a["WRITE_SIZE"][sel]
             byt = (2.0 * fk + wk) * 1024.0
-            dur = summ.get("kernel_durations_ns", {}).get(k, {}).get("avg")
+            dur = summ.get("kernel_durations_ns", {}).get(k, {}).get("timed_dispatch_per_step" if k == "k_loop" else "avg")
             tj = {"kernel": k, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (" + os.path.basename(out) + ")",
                   "FETCH_SIZE_kB_per_dispatch": fk, "WRITE_SIZE_kB_per_dispatch": wk,
                   "correction": "gfx950: FETCH_SIZE counts half of the bytes of wide streaming reads "
