@@ -23,6 +23,20 @@ using namespace bmpc;
 #define BMPC_HOST_CONE_REGS 256
 #endif
 
+#ifdef BMPC_HOST_COUNT_SYNC   // diagnostics: executor barriers and whole-executor reductions per solve
+long long g_syncs = 0, g_reds = 0;
+#define HS_CNT(c) (++(c))
+#else
+#define HS_CNT(c) ((void)0)
+#endif
+extern "C" long long hs_sync_count(int which) {
+#ifdef BMPC_HOST_COUNT_SYNC
+  return which == 0 ? g_syncs : g_reds;
+#else
+  return -1 + 0 * which;
+#endif
+}
+
 namespace {
 template <bool TR, bool CL = true>
 struct HostExecT {
@@ -44,15 +58,15 @@ struct HostExecT {
   double gsum(double v, int) const { return v; }
   double gmax(double v, int) const { return v; }
   double gmin(double v, int) const { return v; }
-  void sync() const {}
+  void sync() const { HS_CNT(g_syncs); }
   bool uniform(bool b) const { return b; }
-  double sum(double v) const { return v; }
-  double max(double v) const { return v; }
-  double min(double v) const { return v; }
+  double sum(double v) const { HS_CNT(g_reds); return v; }
+  double max(double v) const { HS_CNT(g_reds); return v; }
+  double min(double v) const { HS_CNT(g_reds); return v; }
   template <int K>
-  void sum_n(double*) const {}
+  void sum_n(double*) const { HS_CNT(g_reds); }
   template <int K>
-  void min_n(double*) const {}
+  void min_n(double*) const { HS_CNT(g_reds); }
 };
 using HostExec = HostExecT<false>;
 
