@@ -664,6 +664,9 @@ hipError_t launch_blk_kernel(const SolveLaunch& a) {
 template <class M, bool WITH_QP>
 hipError_t launch_solver_blk(const SolveLaunch& a) {
   if (a.qp) return hipErrorInvalidValue;
+#if defined(BMPC_BLK_ALLOW2)   // tools-only A/B: two waves per ego (BMPC_BLOCK_WAVES=2)
+  if (a.nw == 2) return launch_blk_kernel<M, false, 2>(a);
+#endif
   return a.nw == 8 ? launch_blk_kernel<M, false, 8>(a) : launch_blk_kernel<M, false, 4>(a);
 }
 

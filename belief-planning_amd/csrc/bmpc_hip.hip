@@ -638,7 +638,11 @@ static int launch_solve(bmpc_plan* pl, const double* d_x, const double* d_z, con
   const bool blk = B <= blk_max && P.desc.controller == BMPC_CTRL_CVAR;
   if (blk) {
     a.nw = P.T >= BMPC_BLK_WIDE_T ? 8 : 4;
+#if defined(BMPC_BLK_ALLOW2)
+    if (const char* e = getenv("BMPC_BLOCK_WAVES")) a.nw = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : 4;   // tools-only A/B
+#else
     if (const char* e = getenv("BMPC_BLOCK_WAVES")) a.nw = atoi(e) == 8 ? 8 : 4;
+#endif
     a.lds_bytes = solver_lds_bytes_blk(P, xform, a.nw);
     a.rich = true;
     // BMPC_BLK_LDS=0: the small-batch kernel keeps every array in the slab
