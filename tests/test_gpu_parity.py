@@ -154,6 +154,7 @@ def _check_sample_against_oracle(r, N, NB, x, z, xref, tgt, egos, workers=None):
         np.testing.assert_allclose(r["upred"][e, 0], u0, atol=1e-6 if both0 else 5e-3, err_msg=f"ego {e}")
         agree += st == r["status"][e]
         tight += both0
+    print(f"oracle re-solves (N={N} NB={NB}): exit codes agree on {agree} of {len(egos)} sampled egos, both exit 0 on {tight}")
     assert agree >= 0.9 * len(egos), (agree, len(egos))
     return tight
 
