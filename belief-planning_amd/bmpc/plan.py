@@ -198,11 +198,13 @@ class BatchPlan:
     # ---- timing ---------------------------------------------------------------------------
     PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
               "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree", "G_lp", "G_cone", "napplyG",
-              "ts_pre", "ts_bw", "ts_fw", "ts_post", "riccati")
+              "ts_pre", "ts_bw", "ts_fw", "ts_post", "riccati", "coup_ts", "coup_dot", "coup_lu", "lu_solve",
+              "kkt_back")
 
-    def counters(self):
-        """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build)."""
-        out = np.zeros((self.batch, 24))
+    def counters(self, width=24):
+        """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build, whose counter
+        block is 32 wide: pass width=32 for it)."""
+        out = np.zeros((self.batch, width))
         check(lib().bmpc_get_counters(self._h, _p(out)), "bmpc_get_counters")
         return out
 

@@ -250,7 +250,13 @@ enum { MISC_INIT = 0, MISC_JCONS = 1, MISC_OLDU = 2 /* d values */, MISC_BEST = 
 enum {
   PROF_TREE = 0, PROF_RESID, PROF_SCALING, PROF_FACTOR, PROF_COUPLING, PROF_KKT, PROF_TREESOLVE,
   PROF_REFINE, PROF_STEP, PROF_INIT, PROF_TOTAL, PROF_NSOLVE, PROF_APPLYW, PROF_APPLYG, PROF_APPLYGT,
-  PROF_NTREE, PROF_G_LP, PROF_G_CONE, PROF_NAPPLYG, PROF_X1, PROF_X2, PROF_X3, PROF_X4, PROF_COUNT = 24
+  PROF_NTREE, PROF_G_LP, PROF_G_CONE, PROF_NAPPLYG, PROF_X1, PROF_X2, PROF_X3, PROF_X4,
+#if defined(BMPC_PROFILE)
+  // profile builds only (the product's slab keeps 24): the coupling's parts
+  PROF_RIC = 23, PROF_CTS, PROF_CDOT, PROF_LU, PROF_LUS, PROF_BACK, PROF_COUNT = 32
+#else
+  PROF_COUNT = 24
+#endif
 };
 #if defined(BMPC_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {

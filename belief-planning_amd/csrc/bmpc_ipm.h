@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "bmpc_tree.h"
+#include "bmpc_wave.h"
 
 #ifndef BMPC_EQUIL
 #define BMPC_EQUIL 1         // 0: no equilibration (the unscaled IPM of rounds 1-4)
@@ -38,6 +39,15 @@
 #endif
 #ifndef BMPC_BLK_WAVE_SUBST
 #define BMPC_BLK_WAVE_SUBST 1   // multi-wave executors: the coupling substitutions on one wave
+#endif
+#ifndef BMPC_BLK_PAIR_DOTS
+#define BMPC_BLK_PAIR_DOTS 1    // multi-wave executors: the cone-cone coupling block with a lane per (k, j) entry
+#endif
+#ifndef BMPC_BLK_WAVE_LU
+#define BMPC_BLK_WAVE_LU 24     // multi-wave executors: a coupling LU (in LDS) of at most this order on one wave
+#endif
+#ifndef BMPC_SUBST_REG
+#define BMPC_SUBST_REG 1        // the one-wave coupling substitutions with the right-hand side in registers
 #endif
 #ifndef BMPC_REFINE_CALLS
 #define BMPC_REFINE_CALLS 1  // 1: kkt_refine_pair's correction back halves are calls of their own
@@ -143,6 +153,10 @@ BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
   const int k = rnd_ * G.ngrp + G.g < (P).ncones ? rnd_ * G.ngrp + G.g : -1; \
   const int off = k >= 0 ? G##_t.cone_off[k] : 0;                 \
   const int q = k >= 0 ? G##_t.cone_q[k] : 0
+
+// multi-wave executors (the small-batch kernel's DevBlockExecT: one ego on several waves)
+template <class X>
+struct MultiWave : std::integral_constant<bool, (BatchDiv<X>::v > 1)> {};
 
 // ------------------------------------------------------------------------------------
 // block of dot products in one pass: acc[a][b] = sum_i A_a[i] B_b[i] over the tree-variable
@@ -1869,7 +1883,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
     }
     ex.sync();
   }
-  BMPC_TOC(C.ws, L, 23, t_ric);
+  BMPC_TOC(C.ws, L, 23, t_ric);   // PROF_RIC
   return ex.max(bad) == 0.0;
 }
 
@@ -2372,6 +2386,136 @@ BMPC_FN bool small_lu(const X ex, PM* M, PP* piv, int n) {
   return true;
 }
 
+// wave-scope ordering of LDS steps (one wave alone, no workgroup barrier)
+BMPC_HD void wave_sync() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+// small_lu on the first wave of a multi-wave executor alone (small systems, M in LDS): the
+// pivot search as two DPP wave reductions, the steps ordered by wave-scope fences instead of
+// workgroup barriers, the trailing update with a lane per column (conflict-free LDS rows, column
+// k's multipliers broadcast).  The same pivots and the same operation per entry as small_lu.
+// Measured (tools/mb_lu.hip, profiles/r06/r06p_*): per pivot 2,067 vs 2,234 cycles at n = 13,
+// but 3,925 vs 3,019 at n = 46 -- one wave's update chain outweighs the barriers it saves.
+template <class PM, class PP>
+BMPC_HD bool small_lu_wave(int j, PM* M, PP* piv, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int k = 0; k < n; ++k) {
+    const bool live = j >= k && j < n;
+    const double best = live ? fabs(M[j * n + k]) : -1.0;
+    const double amax = dev::wave_reduce<1, true>(best);   // max / min: exact in any order
+    const int p = (int)dev::wave_reduce<2, true>(live && best == amax ? (double)j : 1e300);
+    if (!(amax > 0.0)) return false;
+    if (p != k && j < n) {
+      const double tmp = M[k * n + j];
+      M[k * n + j] = M[p * n + j];
+      M[p * n + j] = tmp;
+    }
+    if (j == 0) piv[k] = (double)p;
+    wave_sync();
+    const double d = M[k * n + k];
+    if (j > k && j < n) M[j * n + k] = M[j * n + k] / d;
+    wave_sync();
+    if (j > k && j < n) {
+      const double mk = M[k * n + j];
+      for (int i0 = k + 1; i0 < n; i0 += 8) {
+        double l[8], a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u < n ? i0 + u : i0;
+          l[u] = M[i * n + k];
+          a[u] = M[i * n + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (i0 + u < n) M[(i0 + u) * n + j] = a[u] - l[u] * mk;
+      }
+    }
+    wave_sync();
+  }
+  return true;
+#else
+  return false;
+#endif
+}
+
+// small_lu_solve on the first wave alone for K right-hand sides with b in registers (lane j: b_j):
+// the row swaps and each substitution step's pivot entry by readlane -- no LDS round trip and no
+// fence on the chain, and K chains interleaved; per right-hand side the same swaps and the same
+// operations in the same order (small_lu_solve, small_lu_solve_rows)
+template <int K, class PM, class PP, class PB>
+BMPC_HD void small_lu_solve_wave(int j, const PM* M, const PP* piv, PB* const (&b)[K], int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  auto bcast = [](double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+  };
+  const bool row = j < n;
+  const size_t rj = (size_t)(row ? j : 0) * n;
+  double bj[K];
+#pragma unroll
+  for (int r = 0; r < K; ++r) bj[r] = row ? (double)b[r][j] : 0.0;
+  for (int k0 = 0; k0 < n; k0 += 8) {   // P
+    double pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pv[u] = piv[k0 + u < n ? k0 + u : k0];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      if (k < n) {
+        const int p = __builtin_amdgcn_readfirstlane((int)pv[u]);
+        if (p != k) {
+#pragma unroll
+          for (int r = 0; r < K; ++r) {
+            const double vk = bcast(bj[r], k), vp = bcast(bj[r], p);
+            if (j == k) bj[r] = vp;
+            if (j == p) bj[r] = vk;
+          }
+        }
+      }
+    }
+  }
+  for (int i0 = 0; i0 < n; i0 += 8) {   // L (unit diagonal)
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i0 + u < n ? i0 + u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < n) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          const double bi = bcast(bj[r], i);
+          if (row && j > i) bj[r] -= mc[u] * bi;
+        }
+      }
+    }
+  }
+  for (int i1 = n - 1; i1 >= 0; i1 -= 8) {   // U
+    double mc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mc[u] = M[rj + (i1 - u >= 0 ? i1 - u : 0)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i1 - u;
+      if (i >= 0) {
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+          if (j == i) bj[r] = bj[r] / mc[u];
+          const double bi = bcast(bj[r], i);
+          if (row && j < i) bj[r] -= mc[u] * bi;
+        }
+      }
+    }
+  }
+  if (row)
+#pragma unroll
+    for (int r = 0; r < K; ++r) b[r][j] = bj[r];
+#endif
+}
+
 template <class X, class = void>
 struct RowLanes : std::false_type {};
 template <class X>
@@ -2421,12 +2565,6 @@ BMPC_HD void small_lu_solve_rows(const X ex, const PM* M, PB* b, int n) {
 // small_lu_solve_rows on the first wave of a multi-wave executor alone: its rows' steps ordered
 // by wave-scope fences instead of one workgroup barrier each (3n barriers per solve; the other
 // waves wait at the caller's one barrier).  Same operations in the same order.
-BMPC_HD void wave_sync() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-#endif
-}
 template <class PM, class PB>
 BMPC_HD void small_lu_solve_rows_wave(int j, const PM* M, PB* b, int n) {
   const bool row = j < n;
@@ -2466,6 +2604,16 @@ BMPC_HD void small_lu_solve_rows_wave(int j, const PM* M, PB* b, int n) {
 // solve with the LU above; b in LDS, column-oriented substitution (one step per row)
 template <class X, class PM, class PP, class PB>
 BMPC_HD void small_lu_solve(const X ex, const PM* M, const PP* piv, PB* b, int n) {
+#if BMPC_SUBST_REG
+  if constexpr (MultiWave<X>::value) {
+    if (n <= 64) {
+      PB* const bs[1] = {b};
+      if (ex.lane < 64) small_lu_solve_wave<1>(ex.lane, M, piv, bs, n);
+      ex.sync();
+      return;
+    }
+  }
+#endif
   if (ex.lane == 0)
     for (int k = 0; k < n; ++k) {
       const int p = (int)piv[k];
@@ -2533,12 +2681,15 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   BMPC_PROF(C.ws, L, PROF_COUPLING);
   gdouble* ws = C.ws;
   const int nc = P.ncones;
+  BMPC_TIC(t_cts);
   if (ex.uniform(nc + extra >= BMPC_TS_POST_RB_MIN))   // NB=2 plans (15 right-hand sides): the batched post-pass
     tree_solve<X, NX, NU, true>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv,
                                 ws + L.colnu, P.neq, nc);
   else
     tree_solve<X, NX, NU>(ex, C, nc + extra, ws + L.gk, P.nv, ws + L.zeros, P.neq, ws + L.colk, P.nv, ws + L.colnu,
                           P.neq, nc);
+  BMPC_TOC(C.ws, L, PROF_CTS, t_cts);
+  BMPC_TIC(t_cdot);
   const int ng = P.ng, nb = P.bdim, ns = P.nsm;
   auto* M = coup_mem(ex, ws, L, P, P.lds_M);
   const gdouble* eta = ws + L.eta;
@@ -2548,7 +2699,32 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   for (int i = ex.lane; i < ns * ns; i += ex.nlanes) M[i] = 0.0;
   ex.sync();
   // cone-cone block: c_k (I/c_k + M) with M[k][j] = g_k' col_j over tree variables
-  if (coup_supp_dots(P)) {   // many cones: over each g_k's support, 16 columns per pass
+  if (coup_supp_dots(P) && BMPC_BLK_PAIR_DOTS && MultiWave<X>::value) {
+    // multi-wave executors (one ego, latency-bound): a lane per entry (k, j), the sum over g_k's
+    // support in order (the host build's order), eight entries' loads in flight -- no reductions
+    const auto t = topo_view(P, ex);
+    for (int pr = ex.lane; pr < nc * nc; pr += ex.nlanes) {
+      const int k = pr / nc, j = pr - (pr / nc) * nc;
+      const gdouble* g = ws + L.gk + (size_t)k * P.nv;
+      const gdouble* v = ws + L.colk + (size_t)j * P.nv;
+      const int tot = cone_supp_len(P, t, k);
+      double acc = 0.0;
+      for (int e0 = 0; e0 < tot; e0 += 8) {
+        double gv[8], vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = cone_supp_idx(P, t, k, e0 + u < tot ? e0 + u : e0);
+          gv[u] = g[i];
+          vv[u] = v[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + u < tot) acc += gv[u] * vv[u];
+      }
+      const double ck = 2.0 / (eta[k] * eta[k]);
+      M[(ng + nb + k) * ns + ng + nb + j] = ck * acc + (k == j ? 1.0 : 0.0);
+    }
+  } else if (coup_supp_dots(P)) {   // many cones: over each g_k's support, 16 columns per pass
     const auto t = topo_view(P, ex);
     for (int k = 0; k < nc; ++k)
       for (int j0 = 0; j0 < nc; j0 += 16) {
@@ -2611,7 +2787,22 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
     M[(ng + nb + k) * ns + i] = -ck * gv;
   }
   ex.sync();
-  return small_lu(ex, M, coup_vec(ex, P.lds_piv), ns);
+  BMPC_TOC(C.ws, L, PROF_CDOT, t_cdot);
+  BMPC_TIC(t_lu);
+  bool ok;
+  if constexpr (MultiWave<X>::value && X::kCoupLds && BMPC_BLK_WAVE_LU > 0) {
+    if (ns <= BMPC_BLK_WAVE_LU && ns <= 64) {
+      double bad = 0.0;
+      if (ex.lane < 64) bad = small_lu_wave(ex.lane, M, coup_vec(ex, P.lds_piv), ns) ? 0.0 : 1.0;
+      ok = ex.max(bad) == 0.0;   // its barrier also hands the factors to the other waves
+    } else {
+      ok = small_lu(ex, M, coup_vec(ex, P.lds_piv), ns);
+    }
+  } else {
+    ok = small_lu(ex, M, coup_vec(ex, P.lds_piv), ns);
+  }
+  BMPC_TOC(C.ws, L, PROF_LU, t_lu);
+  return ok;
 }
 
 template <class X, int NX, int NU, bool R3ZERO>
@@ -2649,6 +2840,7 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
                       gdouble* dx, gdouble* dy, gdouble* dzh, bool fin) {
   CPlan& P = *C.P;
   CLayout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_BACK);
   gdouble* ws = C.ws;
   gdouble* tr = ws + L.k_r0;
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
@@ -2673,7 +2865,9 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
   }
   for (int i = ex.lane; i < ng + nb; i += ex.nlanes) b[i] = i < ng ? tz[gvar(P, i)] : r2[P.T * NX + i - ng];
   ex.sync();
+  BMPC_TIC(t_lus);
   small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b, ns);
+  BMPC_TOC(C.ws, L, PROF_LUS, t_lus);
   const auto* bc = b + ng + nb;
   const gdouble* colk = ws + L.colk;
   const gdouble* colnu = ws + L.colnu;
@@ -2731,6 +2925,7 @@ BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const g
                            const gdouble* r3h2, gdouble* dx2, gdouble* dy2, gdouble* dzh2, bool fin) {
   CPlan& P = *C.P;
   CLayout& L = *C.L;
+  BMPC_PROF(C.ws, L, PROF_BACK);
   gdouble* ws = C.ws;
   gdouble* tr = ws + L.k_r0;
   const int ng = P.ng, nb = P.bdim, nc = P.ncones, ns = P.nsm;
@@ -2766,8 +2961,23 @@ BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const g
     b2[i] = i < ng ? tz2[gvar(P, i)] : r22[P.T * NX + i - ng];
   }
   ex.sync();
-  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b1, ns);
-  small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b2, ns);
+  BMPC_TIC(t_lus);
+  bool both = false;
+#if BMPC_SUBST_REG
+  if constexpr (MultiWave<X>::value) {   // both right-hand sides on one wave, their chains interleaved
+    if (ns <= 64) {
+      decltype(b1) const bs[2] = {b1, b2};
+      if (ex.lane < 64) small_lu_solve_wave<2>(ex.lane, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), bs, ns);
+      ex.sync();
+      both = true;
+    }
+  }
+#endif
+  if (!both) {
+    small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b1, ns);
+    small_lu_solve(ex, coup_mem(ex, ws, L, P, P.lds_M), coup_vec(ex, P.lds_piv), b2, ns);
+  }
+  BMPC_TOC(C.ws, L, PROF_LUS, t_lus);
   const auto* bc1 = b1 + ng + nb;
   const auto* bc2 = b2 + ng + nb;
   const gdouble* colk = ws + L.colk;

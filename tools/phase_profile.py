@@ -23,7 +23,7 @@ def main():
     pl.set_policies(highway_policy_rows(tgt))
     pl.enable_timing(True)
     r0 = pl.solve(x, z, xref)
-    c0 = pl.counters()
+    c0 = pl.counters(32)
     # the profiled solve is the same first solve tools/variant_check.py records (reset: no warm
     # start carried over from the solve above), so its statuses compare with the product's
     pl.reset()
@@ -31,7 +31,7 @@ def main():
     r = pl.solve(x, z, xref)
     assert np.array_equal(r0["status"], r["status"]) and np.array_equal(r0["iters"], r["iters"])
     wall = time.time() - t0
-    c = pl.counters() - c0
+    c = pl.counters(32) - c0
     tm = pl.timing()
     it = r["iters"].astype(float)
     print(f"B={B} N={N} NB={NB} wall {wall*1e3:.1f} ms  k_ipm {tm['ipm_ms']:.2f} ms  k_tree {tm['tree_ms']:.3f} ms"
