@@ -199,7 +199,7 @@ class BatchPlan:
     PHASES = ("tree", "resid", "scaling", "factor", "coupling", "kkt", "treesolve", "refine", "-",
               "init", "total", "nsolve", "applyW", "applyG", "applyGT", "ntree", "G_lp", "G_cone", "napplyG",
               "ts_pre", "ts_bw", "ts_fw", "ts_post", "riccati", "coup_ts", "coup_dot", "coup_lu", "lu_solve",
-              "kkt_back")
+              "kkt_back", "ric_load", "ric_a", "ric_b")
 
     def counters(self, width=24):
         """Per-ego phase cycle counters (non-zero only for a -DBMPC_PROFILE build, whose counter

@@ -253,7 +253,7 @@ enum {
   PROF_NTREE, PROF_G_LP, PROF_G_CONE, PROF_NAPPLYG, PROF_X1, PROF_X2, PROF_X3, PROF_X4,
 #if defined(BMPC_PROFILE)
   // profile builds only (the product's slab keeps 24): the coupling's parts
-  PROF_RIC = 23, PROF_CTS, PROF_CDOT, PROF_LU, PROF_LUS, PROF_BACK, PROF_COUNT = 32
+  PROF_RIC = 23, PROF_CTS, PROF_CDOT, PROF_LU, PROF_LUS, PROF_BACK, PROF_RIC_LD, PROF_RIC_A, PROF_RIC_B, PROF_COUNT = 32
 #else
   PROF_COUNT = 24
 #endif
@@ -275,11 +275,16 @@ struct ProfScope {
   if (threadIdx.x == 0) (ws)[(L).prof + (id)] += (double)(__builtin_amdgcn_s_memtime() - (v))
 #define BMPC_COUNT(ws, L, id) \
   if (threadIdx.x == 0) (ws)[(L).prof + (id)] += 1.0
+// a phase boundary inside a dependent chain: wait for every outstanding load first (profile builds)
+#define BMPC_TOC_WAIT(ws, L, id, v) \
+  __builtin_amdgcn_s_waitcnt(0);      \
+  BMPC_TOC(ws, L, id, v)
 #else
 #define BMPC_PROF(ws, L, id) ((void)0)
 #define BMPC_TIC(v) ((void)0)
 #define BMPC_TOC(ws, L, id, v) ((void)0)
 #define BMPC_COUNT(ws, L, id) ((void)0)
+#define BMPC_TOC_WAIT(ws, L, id, v) ((void)0)
 #endif
 
 // ------------------------------------------------------------------------------------
@@ -508,6 +513,39 @@ BMPC_HD bool chol(double (&L)[D][D]) {
     for (int i = 0; i < j; ++i) L[i][j] = 0.0;
   }
   return true;
+}
+
+// x / y given r = 1 / y (correctly rounded): q0 = x r, then one FMA for the remainder and one
+// for the correction give the correctly rounded quotient (Markstein's theorem; no overflow or
+// underflow in range), so the quotients of a shared divisor cost one division and three
+// operations each instead of a division sequence each -- the same bits as x / y
+// (tools/markstein_check.c: 2e8 random pairs).  The host build divides.
+BMPC_HD double div_rcp(double x, double y, double r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double q0 = x * r;
+  return fma(fma(-q0, y, x), r, q0);
+#else
+  (void)r;
+  return x / y;
+#endif
+}
+// chol_solve with the reciprocals of L's diagonal given (div_rcp): the same bits
+template <int D>
+BMPC_HD void chol_solve_r(const double (&L)[D][D], const double (&ri)[D], double (&b)[D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    double t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= L[i][k] * b[k];
+    b[i] = div_rcp(t, L[i][i], ri[i]);
+  }
+#pragma unroll
+  for (int i = D - 1; i >= 0; --i) {
+    double t = b[i];
+#pragma unroll
+    for (int k = i + 1; k < D; ++k) t -= L[k][i] * b[k];
+    b[i] = div_rcp(t, L[i][i], ri[i]);
+  }
 }
 
 // solve L L' x = b in place

@@ -43,8 +43,11 @@
 #ifndef BMPC_BLK_PAIR_DOTS
 #define BMPC_BLK_PAIR_DOTS 1    // multi-wave executors: the cone-cone coupling block with a lane per (k, j) entry
 #endif
-#ifndef BMPC_BLK_WAVE_LU
-#define BMPC_BLK_WAVE_LU 24     // multi-wave executors: a coupling LU (in LDS) of at most this order on one wave
+#ifndef BMPC_WAVE_LU
+#define BMPC_WAVE_LU 1          // device executors: the coupling LU on one wave over its non-zero rows (small_lu_wave)
+#endif
+#ifndef BMPC_WAVE_LU_MIN1
+#define BMPC_WAVE_LU_MIN1 32    // ... in the one-wave executor from this order on (config 3: 50; multi-wave: always)
 #endif
 #ifndef BMPC_SUBST_REG
 #define BMPC_SUBST_REG 1        // the one-wave coupling substitutions with the right-hand side in registers
@@ -1698,6 +1701,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
       }
       for (int jn = len - 1; jn >= 0; --jn) {
         const int k = ndx + jn, u = ndu + jn;
+        BMPC_TIC(t_rn);
         // this lane's rows of the node's data (independent of the recursion)
         double Hx[RX][NX], Ar[RX][NX], Ac[RX][NX], Br[RX][NU], Hu[NU][NU];
 #pragma unroll
@@ -1749,6 +1753,8 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
             }
           }
         }
+        BMPC_TOC_WAIT(C.ws, L, PROF_RIC_LD, t_rn);
+        BMPC_TIC(t_ra);
         // full A and B (every lane)
         double Af[NX][NX], Bf[NX][NU];
         gather_rows(Ar, Af);
@@ -1810,14 +1816,20 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
             for (int r = 0; r < NX; ++r) v += Bf[r][i] * PBf[r][j];
             Quu[i][j] += v;
           }
+        BMPC_TOC_WAIT(C.ws, L, PROF_RIC_A, t_ra);
+        BMPC_TIC(t_rb);
         if (!chol<NU>(Quu)) bad = 1.0;
+        // the NU + NX column solves share the factor's diagonal: its reciprocals once (div_rcp)
+        double ri[NU];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) ri[i] = 1.0 / Quu[i][i];
         double Qi[NU][NU];   // Quu^-1 (the tree sweeps multiply by it)
 #pragma unroll
         for (int j = 0; j < NU; ++j) {
           double col[NU];
 #pragma unroll
           for (int i = 0; i < NU; ++i) col[i] = i == j ? 1.0 : 0.0;
-          chol_solve<NU>(Quu, col);
+          chol_solve_r<NU>(Quu, ri, col);
 #pragma unroll
           for (int i = 0; i < NU; ++i) Qi[i][j] = col[i];
         }
@@ -1827,7 +1839,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
           double col[NU];
 #pragma unroll
           for (int i = 0; i < NU; ++i) col[i] = -Qux[i][j];
-          chol_solve<NU>(Quu, col);
+          chol_solve_r<NU>(Quu, ri, col);
 #pragma unroll
           for (int i = 0; i < NU; ++i) {
             K[i][j] = col[i];
@@ -1879,6 +1891,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
           }
         }
         if (gl == 0) mat_store(Qi, ws + L.Luu + u * NU * NU);
+        BMPC_TOC_WAIT(C.ws, L, PROF_RIC_B, t_rb);
       }
     }
     ex.sync();
@@ -2393,20 +2406,31 @@ BMPC_HD void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 #endif
 }
-// small_lu on the first wave of a multi-wave executor alone (small systems, M in LDS): the
-// pivot search as two DPP wave reductions, the steps ordered by wave-scope fences instead of
-// workgroup barriers, the trailing update with a lane per column (conflict-free LDS rows, column
-// k's multipliers broadcast).  The same pivots and the same operation per entry as small_lu.
-// Measured (tools/mb_lu.hip, profiles/r06/r06p_*): per pivot 2,067 vs 2,234 cycles at n = 13,
-// but 3,925 vs 3,019 at n = 46 -- one wave's update chain outweighs the barriers it saves.
+// small_lu on one wave (n <= 64; the one-wave executors' own wave, or the first wave of a
+// multi-wave executor): the pivot by one DPP max and a ballot (the smallest row attaining it: the
+// same pivot as small_lu's max-then-min), the trailing update with a lane per column over the
+// rows whose multiplier is non-zero only -- a ballot of column k after the division, since a row
+// with l_i = 0 would get a_ij - 0 * m_kj = a_ij: the coupling system is sparse (a diagonal block of
+// CVaR globals, 3-4 globals per cone), so most pivots update a few rows.  Steps ordered by
+// workgroup-scope fences (the system lives in LDS, or in the slab for lean launches); the same
+// pivots and the same operation per updated entry as small_lu.  Measured (tools/mb_lu.hip,
+// profiles/r06/r06p_*): 2,090 vs 3,057 cycles per pivot on the N=8 NB=2 structure (n = 50),
+// 1,826 vs 2,238 at N=20 NB=1 (n = 14), bit-identical.
+BMPC_HD void lu_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
 template <class PM, class PP>
 BMPC_HD bool small_lu_wave(int j, PM* M, PP* piv, int n) {
 #if defined(__HIP_DEVICE_COMPILE__)
   for (int k = 0; k < n; ++k) {
     const bool live = j >= k && j < n;
     const double best = live ? fabs(M[j * n + k]) : -1.0;
-    const double amax = dev::wave_reduce<1, true>(best);   // max / min: exact in any order
-    const int p = (int)dev::wave_reduce<2, true>(live && best == amax ? (double)j : 1e300);
+    const double amax = dev::wave_reduce<1, true>(best);   // exact in any order
+    const unsigned long long at = __ballot(live && best == amax);
+    const int p = at ? (int)__builtin_ctzll(at) : k;
     if (!(amax > 0.0)) return false;
     if (p != k && j < n) {
       const double tmp = M[k * n + j];
@@ -2414,26 +2438,39 @@ BMPC_HD bool small_lu_wave(int j, PM* M, PP* piv, int n) {
       M[p * n + j] = tmp;
     }
     if (j == 0) piv[k] = (double)p;
-    wave_sync();
+    lu_fence();
     const double d = M[k * n + k];
-    if (j > k && j < n) M[j * n + k] = M[j * n + k] / d;
-    wave_sync();
+    double lj = 0.0;
     if (j > k && j < n) {
-      const double mk = M[k * n + j];
-      for (int i0 = k + 1; i0 < n; i0 += 8) {
+      lj = M[j * n + k] / d;
+      M[j * n + k] = lj;
+    }
+    unsigned long long nz = __ballot(j > k && j < n && lj != 0.0);
+    lu_fence();
+    if (nz) {
+      const bool upd = j > k && j < n;
+      const double mk = upd ? (double)M[k * n + j] : 0.0;
+      while (nz) {
+        int r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          r[u] = nz ? (int)__builtin_ctzll(nz) : -1;
+          nz &= nz ? nz - 1 : 0ull;
+        }
         double l[8], a[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int i = i0 + u < n ? i0 + u : i0;
+          const int i = r[u] >= 0 ? r[u] : r[0];
           l[u] = M[i * n + k];
-          a[u] = M[i * n + j];
+          a[u] = M[i * n + (upd ? j : k)];
         }
+        if (upd)
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (i0 + u < n) M[(i0 + u) * n + j] = a[u] - l[u] * mk;
+          for (int u = 0; u < 8; ++u)
+            if (r[u] >= 0) M[r[u] * n + j] = a[u] - l[u] * mk;
       }
     }
-    wave_sync();
+    lu_fence();
   }
   return true;
 #else
@@ -2790,11 +2827,14 @@ BMPC_FN bool kkt_coupling(const X ex, const Ctx Cin, int extra) {
   BMPC_TOC(C.ws, L, PROF_CDOT, t_cdot);
   BMPC_TIC(t_lu);
   bool ok;
-  if constexpr (MultiWave<X>::value && X::kCoupLds && BMPC_BLK_WAVE_LU > 0) {
-    if (ns <= BMPC_BLK_WAVE_LU && ns <= 64) {
+  // device executors: the one-wave sparse LU -- the multi-wave executor always, the one-wave
+  // executor in lean launches (config 3: n = 50, +2.5%) from BMPC_WAVE_LU_MIN1 on; the LDS-rich
+  // one-wave k_ipm (the headline, n = 14) keeps small_lu's code (-0.2..-0.7% with the other)
+  if constexpr (BMPC_WAVE_LU && RowLanes<X>::value && (MultiWave<X>::value || !X::kCoupLds)) {
+    if (ns <= 64 && (MultiWave<X>::value || ns >= BMPC_WAVE_LU_MIN1)) {
       double bad = 0.0;
       if (ex.lane < 64) bad = small_lu_wave(ex.lane, M, coup_vec(ex, P.lds_piv), ns) ? 0.0 : 1.0;
-      ok = ex.max(bad) == 0.0;   // its barrier also hands the factors to the other waves
+      ok = ex.max(bad) == 0.0;   // a multi-wave executor's barrier also hands the factors to the other waves
     } else {
       ok = small_lu(ex, M, coup_vec(ex, P.lds_piv), ns);
     }
