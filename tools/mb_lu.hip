@@ -313,6 +313,59 @@ __device__ void lu_h4(int lane, ldouble* M, ldouble* piv, int n, ldouble* cand) 
   }
 }
 
+// one wave, the trailing update over the rows whose multiplier is non-zero only (a ballot of
+// column k after the division; a row with l_i = 0 would get a_ij - 0 * m_kj = a_ij), the pivot by
+// one DPP max and a ballot (the smallest row attaining it)
+__device__ bool lu_wsparse(int j, ldouble* M, ldouble* piv, int n) {
+  for (int k = 0; k < n; ++k) {
+    const bool live = j >= k && j < n;
+    const double best = live ? fabs(M[j * n + k]) : -1.0;
+    const double amax = wave_reduce<1>(best);
+    const unsigned long long at = __ballot(live && best == amax);
+    const int p = at ? (int)__builtin_ctzll(at) : k;
+    if (!(amax > 0.0)) return false;
+    if (p != k && j < n) {
+      const double t = M[k * n + j];
+      M[k * n + j] = M[p * n + j];
+      M[p * n + j] = t;
+    }
+    if (j == 0) piv[k] = p;
+    wave_sync();
+    const double d = M[k * n + k];
+    double lj = 0.0;
+    if (j > k && j < n) {
+      lj = M[j * n + k] / d;
+      M[j * n + k] = lj;
+    }
+    unsigned long long nz = __ballot(j > k && j < n && lj != 0.0);
+    wave_sync();
+    if (nz) {
+      const double mk = j > k && j < n ? (double)M[k * n + j] : 0.0;
+      while (nz) {
+        int r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          r[u] = nz ? (int)__builtin_ctzll(nz) : -1;
+          nz &= nz ? nz - 1 : 0ull;
+        }
+        double l[8], a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = r[u] >= 0 ? r[u] : r[0];
+          l[u] = M[i * n + k];
+          a[u] = M[i * n + (j < n ? j : 0)];
+        }
+        if (j > k && j < n)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (r[u] >= 0) M[r[u] * n + j] = a[u] - l[u] * mk;
+      }
+    }
+    wave_sync();
+  }
+  return true;
+}
+
 // permutation + L + U substitutions, b in LDS (lane 0 permutes; rows on lanes, fences)
 __device__ void solve_lds(int j, const ldouble* M, const ldouble* piv, ldouble* b, int n) {
   if (j == 0)
@@ -442,6 +495,9 @@ __global__ void __launch_bounds__(256) k_lu(const double* A, const double* rhs, 
     if constexpr (V == 2) {
       if (lane < 64) lu_wscan(lane, M, piv, n);
     }
+    if constexpr (V == 15) {
+      if (lane < 64) lu_wsparse(lane, M, piv, n);
+    }
     if constexpr (V == 13) lu_h4<2>(lane, M, piv, n, red);
     if constexpr (V == 14) lu_h4<4>(lane, M, piv, n, red);
     if constexpr (V == 7) upd_only<8, 1>(lane, M, n);
@@ -535,6 +591,45 @@ int main(int argc, char** argv) {
     printf("  n=%d  wred == block: %d  wscan == block: %d  solve_reg == solve_lds: %d\n", n,
            (int)(memcmp(r0.data(), r1.data(), r0.size() * 8) == 0), (int)(memcmp(r0.data(), r2.data(), r0.size() * 8) == 0),
            (int)(memcmp(r5.data(), r6.data(), r5.size() * 8) == 0));
+  }
+  // the coupling system's structure (N=8 NB=2: bd = 4 parent branches, m = 3, 13 cones; N=20 NB=1:
+  // bd = 1, 4 cones): globals rho | sigma | mu+ | mu- | J with a diagonal for rho and mu, the CVaR
+  // rows coupling rho_b, sigma_b and mu-_b., the cone block dense, each cone on 3-4 globals
+  for (int cfg = 0; cfg < 2; ++cfg) {
+    const int bd = cfg == 0 ? 4 : 1, m = 3, nc = cfg == 0 ? 13 : 4;
+    const int ng = bd * (2 * m + 2) + 1, n = ng + bd + nc;
+    std::vector<double> A(n * n, 0.0), rhs(n);
+    srand(11);
+    auto rnd = [] { return (double)rand() / RAND_MAX - 0.5; };
+    for (int b = 0; b < bd; ++b) A[b * n + b] = 50.0 + 100.0 * rnd();
+    for (int q = 0; q < 2 * bd * m; ++q) A[(2 * bd + q) * n + 2 * bd + q] = 30.0 + 40.0 * rnd();
+    for (int b = 0; b < bd; ++b) {
+      const int row = ng + b;
+      A[row * n + b] = A[b * n + row] = 1.0;
+      A[row * n + bd + b] = A[(bd + b) * n + row] = 1.0;
+      for (int i = 0; i < m; ++i) {
+        const int gi = 2 * bd + bd * m + b * m + i;
+        A[row * n + gi] = A[gi * n + row] = -0.3 + 0.1 * rnd();
+      }
+    }
+    for (int k = 0; k < nc; ++k) {
+      const int ck = ng + bd + k;
+      for (int j2 = 0; j2 < nc; ++j2) A[ck * n + ng + bd + j2] = (k == j2 ? 1.0 : 0.0) + 0.2 * rnd();
+      const int b = k == nc - 1 ? 0 : k / m % bd, i = k % m;
+      const int gl[4] = {bd + b, 2 * bd + b * m + i, 2 * bd + bd * m + b * m + i, k == nc - 1 ? ng - 1 : b};
+      for (int q = 0; q < 4; ++q) {
+        const double gv = rnd();
+        A[gl[q] * n + ck] = gv;
+        A[ck * n + gl[q]] = -2.0 * gv;
+      }
+    }
+    for (int i = 0; i < n; ++i) rhs[i] = rnd();
+    std::vector<double> s0, s1, s2;
+    printf("structured n=%d\n", n);
+    run<0>("block", n, R, A, rhs, s0, true);
+    run<1>("wred", n, R, A, rhs, s1, true);
+    run<15>("wsparse", n, R, A, rhs, s2, true);
+    printf("  wred == block: %d  wsparse == block: %d\n", (int)(s0 == s1), (int)(s0 == s2));
   }
   // ticks vs wall clock: one long block-LU kernel
   std::vector<double> A(46 * 46), rhs(46), r;
