@@ -14,8 +14,8 @@ static double rnd(int emin, int emax) {
   double v = ldexp(m, e);
   return (xr() & 1) ? -v : v;
 }
-int main(void) {
-  long bad = 0, n = 200000000;
+int main(int argc, char** argv) {
+  long bad = 0, n = argc > 1 ? atol(argv[1]) : 200000000;
   for (long i = 0; i < n; ++i) {
     double x = rnd(-60, 60), y = rnd(-60, 60);
     if (i % 7 == 0) y = ldexp(1.0, (int)(xr() % 40) - 20);   // powers of two
