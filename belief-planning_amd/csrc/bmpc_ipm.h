@@ -161,15 +161,29 @@ BMPC_HD void ctx_qx(const Ctx& C, double (&qx)[NX]) {
 template <class X>
 struct MultiWave : std::integral_constant<bool, (BatchDiv<X>::v > 1)> {};
 
+// e^-beta_k of cone k: the multi-wave executor (one ego, issue-bound) reads the value k_tree stored
+// after the boosts; the batch kernels (HBM-bound: a dependent load costs more than the exp there,
+// headline -2% measured) recompute it -- the same value either way
+template <class X, class PB>
+BMPC_HD double ebeta(const PB* boost, int nc, int k) {
+  if constexpr (MultiWave<X>::value) return boost[nc + k];
+  return exp(-boost[k]);
+}
+
 // ------------------------------------------------------------------------------------
 // block of dot products in one pass: acc[a][b] = sum_i A_a[i] B_b[i] over the tree-variable
 // ranges [lo1, hi1) and [lo2, hi2), rows A_a = A + a*astr (a < na <= 4), B_b = B + b*bstr
 // (b < nb <= 4); every load of a lane's step is issued together (one round trip per pass
 // instead of one per dot product), then each entry is reduced over the wave.
 // ------------------------------------------------------------------------------------
-template <class X>
+// NBR: the B vectors the caller reads (1 or 2: the back halves' g_k' dx), so that the
+// multi-wave executor forms and reduces only those 4 * NBR sums (each sum's reduction is
+// independent of the others: the same bits); the batch kernels keep the sixteen (the trimmed
+// pass cost the headline k_ipm 3.6% -- its register allocation, profiles/r06/r06ad_*)
+template <int NBR0 = 4, class X>
 BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const gdouble* B, size_t bstr, int nb,
                         int lo1, int hi1, int lo2, int hi2, double (&acc)[4][4]) {
+  constexpr int NBR = MultiWave<X>::value ? NBR0 : 4;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -187,9 +201,22 @@ BMPC_HD void block_dots(const X ex, const gdouble* A, size_t astr, int na, const
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += av[a] * bv[b];
+      for (int b = 0; b < (NBR < 4 ? NBR : 4); ++b) acc[a][b] += av[a] * bv[b];
   }
-  ex.template sum_n<16>(&acc[0][0]);   // all sixteen in one reduction (one barrier pair on a multi-wave executor)
+  if constexpr (NBR >= 4) {
+    ex.template sum_n<16>(&acc[0][0]);   // all sixteen in one reduction (one barrier on a multi-wave executor)
+  } else {
+    double v[4 * NBR];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < NBR; ++b) v[a * NBR + b] = acc[a][b];
+    ex.template sum_n<4 * NBR>(v);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < NBR; ++b) acc[a][b] = v[a * NBR + b];
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -499,7 +526,7 @@ BMPC_HD void apply_G_body(const X ex, const Ctx Cin, const gdouble* zv, gdouble*
     const int kk = k >= 0 ? k : 0;
     const int c = k >= 0 ? t.cone_c[kk] : -1;
     const int cb = t.cone_b[kk], ci = t.cone_i[kk];
-    const double ebst = exp(-boost[kk]);
+    const double ebst = ebeta<X>(boost, P.ncones, kk);
     const int c0 = c >= 0 ? c : 0;
     const int ndx = t.br_ndx[c0], ndu = t.br_ndu[c0];
     const bool hasch = t.br_child0[c0] >= 0;
@@ -668,7 +695,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
     const int kc = t.x_cone[k];
     if (kc >= 0) {
       const int off = t.cone_off[kc], q = t.cone_q[kc], j = t.x_conepos[k];
-      const double f = (r[off] - r[off + q - 1]) * exp(-boost[kc]);
+      const double f = (r[off] - r[off + q - 1]) * ebeta<X>(boost, P.ncones, kc);
 #pragma unroll
       for (int s2 = 0; s2 < NX; ++s2) {
         double v = 0.0;
@@ -680,7 +707,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
     } else if (k == 0) {  // root slack in the root cone
       const int kr = P.ncones - 1;
       const int off = t.cone_off[kr], q = t.cone_q[kr];
-      fS = Qs * (r[off] - r[off + q - 1]) * exp(-boost[kr]);
+      fS = Qs * (r[off] - r[off + q - 1]) * ebeta<X>(boost, P.ncones, kr);
     }
     double dhk[NX];
 #pragma unroll
@@ -741,7 +768,7 @@ BMPC_FN_APPLY_GT void apply_GT(const X ex, const Ctx Cin, const gdouble* r, gdou
         if (gi == P.oJ) w -= 1.0;
         if (gi == P.oRho) w += 1.0;
       }
-      if (w != 0.0) v += w * (r[off] - r[off + q - 1]) * exp(-boost[k]);
+      if (w != 0.0) v += w * (r[off] - r[off + q - 1]) * ebeta<X>(boost, P.ncones, k);
     }
     out[gi] = v + sa * ad[gi];
   }
@@ -1611,7 +1638,7 @@ BMPC_FN bool kkt_factor(const X ex, const Ctx Cin, bool zero_g) {
   for (int k = 0; k < P.ncones; ++k) {
     gdouble* g = ws + L.gk + (size_t)k * P.nv;
     const int off = t.cone_off[k], q = t.cone_q[k], c = t.cone_c[k];
-    const double kap = (wb[off] + wb[off + q - 1]) * exp(-boost[k]);
+    const double kap = (wb[off] + wb[off + q - 1]) * ebeta<X>(boost, P.ncones, k);
     if (c >= 0) {
       for (int it = ex.lane; it < P.N; it += ex.nlanes) {
         const int xk = t.br_ndx[c] + it, uk = t.br_ndu[c] + it;
@@ -2898,7 +2925,7 @@ BMPC_HD void kkt_back(const X ex, const Ctx& C, const gdouble* tz, const gdouble
     for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx, four cones per pass
       const int na = nc - k0 < 4 ? nc - k0 : 4;
       double acc[4][4];
-      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
+      block_dots<1>(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx, 0, 1, 0, P.oRho, P.oS, P.oJ, acc);
       if (ex.lane == 0)
         for (int a = 0; a < na; ++a) b[ng + nb + k0 + a] = 2.0 / (eta[k0 + a] * eta[k0 + a]) * acc[a][0];
     }
@@ -2987,7 +3014,7 @@ BMPC_HD void kkt_back_pair(const X ex, const Ctx& C, const gdouble* tz1, const g
     for (int k0 = 0; k0 < nc; k0 += 4) {   // g_k' dx1 and g_k' dx2, four cones per pass
       const int na = nc - k0 < 4 ? nc - k0 : 4;
       double acc[4][4];
-      block_dots(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx1, (size_t)(dx2 - dx1), 2, 0, P.oRho, P.oS, P.oJ,
+      block_dots<2>(ex, ws + L.gk + (size_t)k0 * P.nv, P.nv, na, dx1, (size_t)(dx2 - dx1), 2, 0, P.oRho, P.oS, P.oJ,
                  acc);
       if (ex.lane == 0)
         for (int a = 0; a < na; ++a) {

@@ -393,7 +393,7 @@ std::string build_plan(const bmpc_plan_desc& desc, HostPlan& hp) {
   L.w = take(nbr);
   L.p = take((size_t)bd * m);
   L.dp = take((size_t)bd * m * n);
-  L.boost = take(nc);
+  L.boost = take(2 * (size_t)nc);   // the cone boosts beta_k, then e^-beta_k
   L.xref = take(n);
   L.x = take(nv);
   L.y = take(neq);

@@ -163,6 +163,7 @@ BMPC_HD void tree_update(const X& ex, const Plan& P, const Layout& L, EgoView E,
       }
     }
     boost[k] = BMPC_CONE_BOOST ? 0.5 * log(est > 1.0 ? est : 1.0) : 0.0;
+    boost[P.ncones + k] = exp(-boost[k]);   // e^-beta, read by the IPM's operators (the same value)
   }
   ex.sync();
 }
